@@ -1,0 +1,215 @@
+/*
+ * tiledb_amd.h -- C-ABI of the MI355X-native TileDB tile unfilter engine.
+ *
+ * Drop-in boundary for TileDB's read path:
+ *   ReaderBase::unfilter_tile -> FilterPipeline::run_reverse
+ *   (reference: tiledb/sm/query/readers/reader_base.cc:1075,1094,1118 and
+ *    tiledb/sm/filter/filter_pipeline.h:250-258 / filter_pipeline.cc:439-517)
+ * The contract that survives the swap is the on-disk byte layout
+ * (format_spec/tile.md, format_spec/filter_pipeline.md): the engine consumes
+ * the serialized pipeline descriptor exactly as FilterPipeline::serialize
+ * writes it, and whole filtered tiles exactly as they sit on disk.
+ *
+ * Every function returns a tdbg_status (0 = OK) and never throws.  The last
+ * error message of the calling thread is available through
+ * tdbg_last_error().  Plain pointers and sizes only; no torch types.
+ */
+#ifndef TILEDB_AMD_H
+#define TILEDB_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- on-disk codes (tiledb/api/c_api/filter/filter_api_enum.h:27-69) ---- */
+enum tdbg_filter_type {
+  TDBG_FILTER_NONE = 0,
+  TDBG_FILTER_GZIP = 1,
+  TDBG_FILTER_ZSTD = 2,
+  TDBG_FILTER_LZ4 = 3,
+  TDBG_FILTER_RLE = 4,
+  TDBG_FILTER_BZIP2 = 5,
+  TDBG_FILTER_DOUBLE_DELTA = 6,
+  TDBG_FILTER_BIT_WIDTH_REDUCTION = 7,
+  TDBG_FILTER_BITSHUFFLE = 8,
+  TDBG_FILTER_BYTESHUFFLE = 9,
+  TDBG_FILTER_POSITIVE_DELTA = 10,
+  TDBG_FILTER_AES_256_GCM = 11, /* internal (filter_type.h:17) */
+  TDBG_FILTER_CHECKSUM_MD5 = 12,
+  TDBG_FILTER_CHECKSUM_SHA256 = 13,
+  TDBG_FILTER_DICTIONARY = 14,
+  TDBG_FILTER_SCALE_FLOAT = 15,
+  TDBG_FILTER_XOR = 16,
+  TDBG_FILTER_DEPRECATED = 17,
+  TDBG_FILTER_WEBP = 18,
+  TDBG_FILTER_DELTA = 19
+};
+
+/* tiledb/sm/enums/compressor.h:51-67 */
+enum tdbg_compressor {
+  TDBG_COMPRESSOR_NONE = 0,
+  TDBG_COMPRESSOR_GZIP = 1,
+  TDBG_COMPRESSOR_ZSTD = 2,
+  TDBG_COMPRESSOR_LZ4 = 3,
+  TDBG_COMPRESSOR_RLE = 4,
+  TDBG_COMPRESSOR_BZIP2 = 5,
+  TDBG_COMPRESSOR_DOUBLE_DELTA = 6,
+  TDBG_COMPRESSOR_DICTIONARY = 7,
+  TDBG_COMPRESSOR_DELTA = 8
+};
+
+/* tiledb/api/c_api/datatype/datatype_api_enum.h:34-120 (subset named) */
+enum tdbg_datatype {
+  TDBG_INT32 = 0,
+  TDBG_INT64 = 1,
+  TDBG_FLOAT32 = 2,
+  TDBG_FLOAT64 = 3,
+  TDBG_CHAR = 4,
+  TDBG_INT8 = 5,
+  TDBG_UINT8 = 6,
+  TDBG_INT16 = 7,
+  TDBG_UINT16 = 8,
+  TDBG_UINT32 = 9,
+  TDBG_UINT64 = 10,
+  TDBG_STRING_ASCII = 11,
+  TDBG_STRING_UTF8 = 12,
+  TDBG_STRING_UTF16 = 13,
+  TDBG_STRING_UTF32 = 14,
+  TDBG_STRING_UCS2 = 15,
+  TDBG_STRING_UCS4 = 16,
+  TDBG_ANY = 17,
+  TDBG_DATETIME_YEAR = 18, /* ... DATETIME_AS = 30 */
+  TDBG_DATETIME_AS = 30,
+  TDBG_TIME_HR = 31, /* ... TIME_AS = 39 */
+  TDBG_TIME_AS = 39,
+  TDBG_BLOB = 40,
+  TDBG_BOOL = 41,
+  TDBG_GEOM_WKB = 42,
+  TDBG_GEOM_WKT = 43
+};
+
+/* ---- status codes: one per distinct reference failure class ---- */
+enum tdbg_status {
+  TDBG_OK = 0,
+  TDBG_E_ARG = 1,           /* invalid argument / null pointer                */
+  TDBG_E_TILE_FORMAT = 2,   /* chunk directory runs past the tile (Deserializer) */
+  TDBG_E_TILE_SIZE = 3,     /* "Incorrect unfiltered tile size allocated." tile.cc:308 */
+  TDBG_E_MD_READ = 4,       /* FilterBuffer::read past end of chunk metadata   */
+  TDBG_E_DATA_READ = 5,     /* filter input read past end (get_const_buffer/read) */
+  TDBG_E_OUT_FULL = 6,      /* output full / fixed allocation too small        */
+  TDBG_E_RLE_FORMAT = 7,    /* RLE "invalid input buffer format" rle_compressor.cc:120 */
+  TDBG_E_DD_TYPE = 8,       /* DoubleDelta float / unsupported type dd_compressor.cc:195 */
+  TDBG_E_BWR_BITS = 9,      /* BWR compressed-bits field not 8/16/32/64        */
+  TDBG_E_UNSUPPORTED = 10,  /* filter/pipeline not handled by this engine       */
+  TDBG_E_SCRATCH = 11,      /* internal: stage larger than scratch (retried)   */
+  TDBG_E_PD_DECREASING = 12,/* forward only: "delta is not positive"           */
+  TDBG_E_DD_OVERFLOW = 13,  /* forward only: delta exceeds int64               */
+  TDBG_E_DEVICE = 14,       /* HIP runtime error                               */
+  TDBG_E_DESCRIPTOR = 15    /* malformed serialized pipeline                    */
+};
+
+/* unfilter flags */
+#define TDBG_TILE_OFFSETS 0x1u /* offsets tile: expected size = out_size - 8 (tile.cc:241-248) */
+
+typedef struct tdbg_pipeline tdbg_pipeline; /* immutable, shareable */
+typedef struct tdbg_context tdbg_context;   /* per (device, host thread) */
+typedef void* tdbg_stream;                  /* hipStream_t */
+
+/* Message of the calling thread's last failure; returns bytes written. */
+size_t tdbg_last_error(char* buf, size_t cap);
+const char* tdbg_status_str(int status);
+
+/* Parse the serialized pipeline exactly as FilterPipeline::deserialize
+ * (filter_pipeline.cc:544-557, filter_create.cc:100-201) and assign each
+ * filter its datatype along the chain starting at on_disk_datatype
+ * (filter_pipeline.cc:80-88).  cell_size = Tile::cell_size() (RLE value width,
+ * compression_filter.cc:357,418). */
+int tdbg_pipeline_create(const uint8_t* serialized, size_t len,
+                         uint32_t format_version, uint8_t on_disk_datatype,
+                         uint64_t cell_size, tdbg_pipeline** out);
+void tdbg_pipeline_destroy(tdbg_pipeline* p);
+/* 1 if every filter runs on the engine, 0 if the caller must keep its own CPU
+ * path (checksum, encryption, gzip/zstd/lz4/bzip2, dictionary, xor, float
+ * scale, webp, delta). */
+int tdbg_pipeline_supported(const tdbg_pipeline* p);
+uint32_t tdbg_pipeline_num_filters(const tdbg_pipeline* p);
+/* Filter i: type code and the datatype assigned by the chain. */
+int tdbg_pipeline_filter(const tdbg_pipeline* p, uint32_t i, uint8_t* type,
+                         uint8_t* datatype);
+
+/* Per-device execution context (scratch, status arrays, streams). */
+int tdbg_context_create(int device, tdbg_context** out);
+void tdbg_context_destroy(tdbg_context* ctx);
+
+/* Device-resident batch unfilter: the replacement for the
+ * parallel_for_2d(tile, range) -> FilterPipeline::run_reverse loop of
+ * ReaderBase::unfilter_tiles (reader_base.cc:966-989).
+ *   d_filtered[i] / d_filtered_size[i]: filtered tile i in device memory
+ *   d_out[i] / d_out_size[i]: caller-allocated unfiltered buffer (device)
+ *   d_status[i]: per-tile tdbg_status written by the device (may be NULL)
+ * All four arrays live in device memory on ctx's device.  Enqueues on stream
+ * and returns without synchronizing; per-tile failures are reported through
+ * d_status (TDBG_E_SCRATCH means "re-run with tdbg_unfilter_tiles_sync"). */
+int tdbg_unfilter_tiles_async(tdbg_context* ctx, const tdbg_pipeline* p,
+                              uint64_t ntiles,
+                              const uint8_t* const* d_filtered,
+                              const uint64_t* d_filtered_size,
+                              uint8_t* const* d_out,
+                              const uint64_t* d_out_size, uint32_t flags,
+                              int32_t* d_status, tdbg_stream stream);
+
+/* Same, synchronous: resolves TDBG_E_SCRATCH tiles with the global-memory
+ * path, copies the statuses to host_status (may be NULL) and returns the
+ * first failing tile's status, like parallel_for_2d keeps the first error
+ * (parallel_functions.h:340-345). */
+int tdbg_unfilter_tiles_sync(tdbg_context* ctx, const tdbg_pipeline* p,
+                             uint64_t ntiles, const uint8_t* const* d_filtered,
+                             const uint64_t* d_filtered_size,
+                             uint8_t* const* d_out, const uint64_t* d_out_size,
+                             uint32_t flags, int32_t* host_status,
+                             tdbg_stream stream);
+
+/* Host-resident end-to-end: tiles start in host memory (as FilteredData
+ * leaves them, filtered_data.h:397-398) and end in host result buffers.
+ * Pinned staging + hipMemcpyAsync H2D / unfilter / D2H on ctx's device,
+ * double-buffered over batches of batch_bytes. */
+int tdbg_unfilter_tiles_host(tdbg_context* ctx, const tdbg_pipeline* p,
+                             uint64_t ntiles, const uint8_t* const* filtered,
+                             const uint64_t* filtered_size, uint8_t* const* out,
+                             const uint64_t* out_size, uint32_t flags,
+                             int32_t* host_status, uint64_t batch_bytes);
+
+/* Multi-GPU host-resident end-to-end: tiles are sharded over devices by
+ * contiguous ranges balanced by bytes, one host thread + context per device,
+ * no inter-GPU communication. */
+int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
+                                  const uint8_t* const* filtered,
+                                  const uint64_t* filtered_size,
+                                  uint8_t* const* out,
+                                  const uint64_t* out_size, uint32_t flags,
+                                  int32_t* host_status, const int* devices,
+                                  int ndevices, uint64_t batch_bytes);
+
+/* Stats mirrored from the reference (filter_pipeline.cc:490-491,
+ * reader_base.cc:1074): cumulative since context creation. */
+int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
+                       uint64_t* read_unfiltered_byte_num);
+
+/* Device-side timing of the last tdbg_unfilter_tiles_* launch on ctx, via
+ * hipEvents recorded around the kernel on its stream (ms). */
+int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
+
+/* Device memory helpers for FFI callers without their own allocator. */
+int tdbg_device_alloc(int device, uint64_t bytes, void** out);
+int tdbg_device_free(void* p);
+int tdbg_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
+int tdbg_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+int tdbg_device_count(int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TILEDB_AMD_H */

@@ -1,0 +1,226 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Bit-exact for every byte and identical status codes, on the BASELINE configs
+at test sizes, the SURVEY A.5 edge cases, random pipelines and corrupted
+tiles; plus full-size round-trip properties at the BASELINE tile counts.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from tests.cases import config_cases, edge_cases, random_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from tiledb_amd import engine
+    return engine
+
+
+@pytest.fixture(scope="module")
+def ctx(eng):
+    return eng.Context(0)
+
+
+def encode(O, case):
+    op = O.OraclePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    enc = []
+    for i, t in enumerate(case.tiles):
+        offs = case.offsets[i] if case.offsets else None
+        try:
+            f = op.filter_tile(t, offs, case.max_chunk)
+        except O.OracleError:
+            continue
+        osz = t.size + (8 if case.offsets_tile else 0)
+        enc.append((np.frombuffer(f, dtype=np.uint8), t, osz))
+    return op, enc
+
+
+def check_parity(eng, ctx, O, case, filtered, out_sizes, originals=None, fill=0):
+    op = O.OraclePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    assert dp.supported
+    batch = eng.TileBatch.from_host(filtered, out_sizes, fill=fill)
+    st = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile)
+    out = batch.outputs_host()
+    for i, f in enumerate(filtered):
+        rc, ref = op.unfilter_tile(f, out_sizes[i], case.offsets_tile, fill=fill)
+        assert int(st[i]) == rc, f"{case.name} tile {i}: gpu status {st[i]} oracle {rc}"
+        if rc == 0:
+            o = int(batch.out_off[i])
+            got = out[o:o + out_sizes[i]]
+            if not np.array_equal(got, ref):
+                bad = np.nonzero(got != ref)[0]
+                raise AssertionError(f"{case.name} tile {i}: {bad.size} bytes differ, first at "
+                                     f"{bad[0]} gpu {got[bad[0]]} oracle {ref[bad[0]]}")
+            if originals is not None and originals[i] is not None:
+                n = originals[i].size
+                if np.array_equal(ref[:n], originals[i]):
+                    assert np.array_equal(got[:n], originals[i])
+    return st
+
+
+_CONFIG = config_cases(4)
+_EDGE = edge_cases()
+_RANDOM = random_cases(120)
+
+
+@pytest.mark.parametrize("case", _CONFIG, ids=[c.name for c in _CONFIG])
+def test_config_parity(eng, ctx, oracle_mod, case):
+    _, enc = encode(oracle_mod, case)
+    assert enc
+    check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc],
+                 [e[1] for e in enc])
+
+
+@pytest.mark.parametrize("case", _EDGE, ids=[c.name for c in _EDGE])
+def test_edge_parity(eng, ctx, oracle_mod, case):
+    _, enc = encode(oracle_mod, case)
+    if not enc:
+        pytest.skip("reference encoder rejects this input")
+    check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc],
+                 [e[1] for e in enc])
+
+
+def test_random_pipelines_parity(eng, ctx, oracle_mod):
+    n = 0
+    for case in _RANDOM:
+        _, enc = encode(oracle_mod, case)
+        if not enc:
+            continue
+        check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc],
+                     [e[1] for e in enc])
+        n += 1
+    assert n > 60
+
+
+def _mutations(f: np.ndarray, rng):
+    """Corruptions of an on-disk tile: truncation, header/metadata byte flips."""
+    out = []
+    out.append(f[: max(0, f.size - 1)])
+    out.append(f[: f.size // 2])
+    out.append(f[:7])
+    g = f.copy(); g[0] ^= 3; out.append(g)                          # nchunks
+    if f.size > 12:
+        g = f.copy(); g[8] ^= 1; out.append(g)                      # orig size
+        g = f.copy(); g[12] ^= 0x40; out.append(g)                  # filtered size
+        g = f.copy(); g[16] ^= 0x10; out.append(g)                  # md size
+    for _ in range(6):
+        if f.size > 24:
+            g = f.copy()
+            k = int(rng.integers(20, min(f.size, 120)))
+            g[k] ^= np.uint8(1 << int(rng.integers(8)))
+            out.append(g)
+    return out
+
+
+@pytest.mark.parametrize("case", _CONFIG + [c for c in _EDGE if c.name.startswith(("dd_", "rle_run_65535",
+                                                                                    "bwr_window_437",
+                                                                                    "pd_", "bwr_then",
+                                                                                    "byte_bit"))],
+                         ids=lambda c: c.name)
+def test_corrupt_tiles_status_parity(eng, ctx, oracle_mod, case):
+    rng = np.random.default_rng(7)
+    _, enc = encode(oracle_mod, case)
+    if not enc:
+        pytest.skip("reference encoder rejects this input")
+    f, t, osz = enc[0]
+    muts = _mutations(f, rng)
+    check_parity(eng, ctx, oracle_mod, case, muts, [osz] * len(muts), fill=0x5A)
+
+
+def test_wrong_output_size(eng, ctx, oracle_mod):
+    case = _CONFIG[-2]
+    _, enc = encode(oracle_mod, case)
+    f, t, osz = enc[0]
+    check_parity(eng, ctx, oracle_mod, case, [f, f, f], [osz - 4, osz + 4, 0])
+
+
+def test_full_size_c5_roundtrip(eng, ctx, oracle_mod):
+    """BASELINE C5 per-GPU shard (12,500 tiles x 64 KiB), ramp+rand mixed:
+    size-independent property = the unfiltered bytes equal the written tiles."""
+    from tests.cases import c5_tiles, P, DD
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
+    case_p = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
+    op = oracle_mod.OraclePipeline(case_p.serialize(), 23, int(Datatype.INT32), 4)
+    uniq = c5_tiles(48, "ramp") + c5_tiles(16, "rand")
+    enc = [np.frombuffer(op.filter_tile(t), dtype=np.uint8) for t in uniq]
+    ntiles = 12500
+    idx = np.arange(ntiles) % len(enc)
+    tiles = [enc[i] for i in idx]
+    dp = eng.DevicePipeline(case_p.serialize(), 23, int(Datatype.INT32), 4)
+    batch = eng.TileBatch.from_host(tiles, [65536] * ntiles)
+    st = ctx.unfilter(dp, batch)
+    assert not st.any()
+    out = batch.outputs_host().reshape(ntiles, 65536)
+    for k in range(len(enc)):
+        rows = out[idx == k]
+        assert (rows == uniq[k][None, :]).all()
+
+
+def test_host_end_to_end_and_multi_gpu(eng, ctx, oracle_mod):
+    import torch
+    case = _CONFIG[-1]
+    _, enc = encode(oracle_mod, case)
+    filtered = [e[0] for e in enc] * 8
+    origs = [e[1] for e in enc] * 8
+    osz = [e[2] for e in enc] * 8
+    # pinned host buffers, contiguous (FilteredData-style batch)
+    sizes = np.array([f.size for f in filtered], dtype=np.uint64)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    hin = torch.empty(int(sizes.sum()), dtype=torch.uint8).pin_memory()
+    hin_np = hin.numpy()
+    for f, o in zip(filtered, offs):
+        hin_np[int(o):int(o) + f.size] = f
+    osz_a = np.array(osz, dtype=np.uint64)
+    ooff = np.zeros_like(osz_a)
+    ooff[1:] = np.cumsum(osz_a)[:-1]
+    hout = torch.zeros(int(osz_a.sum()), dtype=torch.uint8).pin_memory()
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    in_ptrs = offs + np.uint64(hin.data_ptr())
+    out_ptrs = ooff + np.uint64(hout.data_ptr())
+    st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz_a, batch_bytes=3 * 65536)
+    assert not st.any()
+    res = hout.numpy()
+    for i, o in enumerate(origs):
+        assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
+    hout.zero_()
+    st = eng.unfilter_multi_gpu(dp, in_ptrs, sizes, out_ptrs, osz_a, [0, 0], batch_bytes=1 << 20)
+    assert not st.any()
+    res = hout.numpy()
+    for i, o in enumerate(origs):
+        assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
+
+
+def test_async_api_and_timing(eng, ctx, oracle_mod):
+    import torch
+    case = _CONFIG[0]
+    _, enc = encode(oracle_mod, case)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    batch = eng.TileBatch.from_host([e[0] for e in enc], [e[2] for e in enc])
+    ctx.unfilter_async(dp, batch)
+    torch.cuda.synchronize()
+    assert not batch.d_status.cpu().numpy().any()
+    assert ctx.last_kernel_ms() > 0
+    out = batch.outputs_host()
+    for i, e in enumerate(enc):
+        o = int(batch.out_off[i])
+        assert np.array_equal(out[o:o + e[1].size], e[1])
+
+
+def test_filter_pipeline_run_reverse_api(eng, oracle_mod):
+    """FilterPipeline.run_reverse mirror raises FilterStatusException like the reference."""
+    from tiledb_amd.filter_pipeline import FilterStatusException
+    case = _CONFIG[4]
+    _, enc = encode(oracle_mod, case)
+    f, t, osz = enc[0]
+    batch = case.pipeline.run_reverse([f], [osz], case.dtype, case.cell_size)
+    assert np.array_equal(batch.output(0), t)
+    with pytest.raises(FilterStatusException):
+        case.pipeline.run_reverse([f[:100]], [osz], case.dtype, case.cell_size)

@@ -1,0 +1,75 @@
+"""ctypes binding of libtiledb_amd.so (the C-ABI in include/tiledb_amd.h).
+
+The library is built in-tree by tiledb_amd/build.py (hipcc, gfx950).  There is
+no CPU fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # torch ships its own libamdhip64; load it first so one HIP runtime is used
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for pure C-ABI use
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtiledb_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build the HIP engine with `python tiledb_amd/build.py` "
+        "(or __graft_entry__.build()); there is no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/tiledb_amd.h exactly
+SIGNATURES = {
+    "tdbg_last_error": (ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t]),
+    "tdbg_status_str": (ctypes.c_char_p, [ctypes.c_int]),
+    "tdbg_pipeline_create": (ctypes.c_int, [c_u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint8,
+                                            ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "tdbg_pipeline_destroy": (None, [c_vp]),
+    "tdbg_pipeline_supported": (ctypes.c_int, [c_vp]),
+    "tdbg_pipeline_num_filters": (ctypes.c_uint32, [c_vp]),
+    "tdbg_pipeline_filter": (ctypes.c_int, [c_vp, ctypes.c_uint32, c_u8p, c_u8p]),
+    "tdbg_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "tdbg_context_destroy": (None, [c_vp]),
+    "tdbg_unfilter_tiles_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                                                 ctypes.c_uint32, c_vp, c_vp]),
+    "tdbg_unfilter_tiles_sync": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                                                ctypes.c_uint32, c_i32p, c_vp]),
+    "tdbg_unfilter_tiles_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                                                ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
+    "tdbg_unfilter_tiles_multi_gpu": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                                                     ctypes.c_uint32, c_i32p,
+                                                     ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                                     ctypes.c_uint64]),
+    "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
+    "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
+    "tdbg_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "tdbg_device_free": (ctypes.c_int, [c_vp]),
+    "tdbg_memcpy_h2d": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
+    "tdbg_memcpy_d2h": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
+    "tdbg_device_count": (ctypes.c_int, [c_i32p]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(1024)
+    lib.tdbg_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def status_str(code: int) -> str:
+    return lib.tdbg_status_str(code).decode()

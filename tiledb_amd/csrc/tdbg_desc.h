@@ -1,0 +1,62 @@
+// tdbg_desc.h -- pipeline plan shared by the host orchestration
+// (tdbg_host.cpp) and the gfx950 kernels (tdbg_kernels.hip).
+//
+// The host resolves every filter of a deserialized FilterPipeline into a
+// "stage kind" plus the integer widths the reference picks at run time
+// (bit_width_reduction_filter.cc:288-350, positive_delta_filter.cc:262-322,
+// dd_compressor.cc:131-200, compression_filter.cc:357,418), so the device
+// never switches on datatypes.
+#pragma once
+#include <stdint.h>
+
+#define TDBG_MAX_FILTERS 16
+
+enum tdbg_stage_kind : uint8_t {
+  TDBG_K_PASS = 0,        // append_view pass-through (NOOP, NONE, BWR/PD on non-int)
+  TDBG_K_BYTESHUFFLE = 1, // ByteshuffleFilter::run_reverse
+  TDBG_K_BITSHUFFLE = 2,  // BitshuffleFilter::run_reverse
+  TDBG_K_BWR = 3,         // BitWidthReductionFilter::run_reverse<T>
+  TDBG_K_PD = 4,          // PositiveDeltaFilter::run_reverse<T>
+  TDBG_K_DD = 5,          // CompressionFilter + DoubleDelta::decompress<T>
+  TDBG_K_RLE = 6,         // CompressionFilter + RLE::decompress
+  TDBG_K_UNSUPPORTED = 7
+};
+
+struct tdbg_stage {
+  uint8_t kind;
+  uint8_t w;    // element width: BWR/PD T, DD T (0 = DD type error), shuffle ts
+  uint8_t sgn;  // T signed (BWR sign extension)
+  uint8_t dts;  // datatype_size(filter datatype): md offset / output value width
+  uint32_t window;
+  uint64_t cs;  // RLE value size (Tile::cell_size)
+};
+
+struct tdbg_plan {
+  uint32_t nstages;
+  uint32_t fast;  // fused fast-path selector (tdbg_fast_kind), 0 = none
+  tdbg_stage s[TDBG_MAX_FILTERS];
+};
+
+enum tdbg_fast_kind : uint32_t {
+  TDBG_FAST_NONE = 0,
+};
+
+namespace tdbg {
+// kernel parameters (passed by value)
+struct KParams {
+  const uint8_t* const* in;
+  const uint64_t* in_size;
+  uint8_t* const* out;
+  const uint64_t* out_size;
+  int32_t* status;
+  uint64_t* need;            // per-tile scratch requirement on TDBG_E_SCRATCH
+  const uint32_t* tile_list; // optional indirection (retry pass)
+  uint64_t ntiles;
+  uint32_t flags;
+  uint8_t* scratch;
+  uint64_t slot_bytes;
+  uint32_t slot_cap, md_cap, tab_cap;
+  tdbg_plan plan;
+};
+
+}  // namespace tdbg

@@ -1,0 +1,242 @@
+// tdbg_device.h -- device helpers for the gfx950 unfilter kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tiledb_amd.h"
+
+#define GEN_NT 256  // threads per workgroup, general interpreter (4 wave64)
+#define DD_EPT 8    // double-delta elements per thread per round
+
+namespace tdbg {
+
+// ---- byte access at arbitrary alignment ----------------------------------
+// Loads k (1..8) little-endian bytes at p.  Only dwords that contain a
+// requested byte are touched, so a read never crosses into a page that holds
+// none of the requested bytes (safe at the end of a global allocation).
+__device__ __forceinline__ uint64_t ldn(const uint8_t* p, uint32_t k) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t nd = (sh + k + 3) >> 2;
+  const uint32_t d0 = q[0];
+  const uint32_t d1 = nd > 1 ? q[1] : 0u;
+  const uint32_t d2 = nd > 2 ? q[2] : 0u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  uint64_t v = ((uint64_t)hi << 32) | lo;
+  if (k < 8) v &= (1ull << (8 * k)) - 1;
+  return v;
+}
+
+__device__ __forceinline__ void stn(uint8_t* p, uint64_t v, uint32_t k) {
+  const uintptr_t a = (uintptr_t)p;
+  if (k == 8 && (a & 7) == 0) { *(uint64_t*)p = v; return; }
+  if (k == 4 && (a & 3) == 0) { *(uint32_t*)p = (uint32_t)v; return; }
+  if (k == 2 && (a & 1) == 0) { *(uint16_t*)p = (uint16_t)v; return; }
+  for (uint32_t i = 0; i < k; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+__host__ __device__ __forceinline__ uint64_t wmask(uint32_t w) {
+  return w >= 8 ? ~0ull : ((1ull << (8 * w)) - 1);
+}
+__host__ __device__ __forceinline__ int64_t sext64(uint64_t v, uint32_t w) {
+  if (w >= 8) return (int64_t)v;
+  const uint32_t s = 64 - 8 * w;
+  return (int64_t)(v << s) >> s;
+}
+
+// 8x8 bit-matrix transpose: bit (8i+j) <-> bit (8j+i) (Hacker's Delight).
+__host__ __device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
+  uint64_t t;
+  t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x = x ^ t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x = x ^ t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  x = x ^ t ^ (t << 28);
+  return x;
+}
+
+// ---- wave64 / block scans --------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incscan_u64(uint64_t x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  return x;
+}
+
+// Exclusive block scan of one u64 per thread; red >= NT/64 entries of LDS.
+template <int NT = GEN_NT>
+__device__ __forceinline__ uint64_t block_exscan_u64(uint64_t v, uint64_t& total,
+                                                     uint64_t* red) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t inc = wave_incscan_u64(v);
+  if (lane == 63) red[wid] = inc;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const uint64_t s = red[i];
+    if ((uint32_t)i < wid) pre += s;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + inc - v;
+}
+
+template <int NT = GEN_NT>
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t y = __shfl_xor(v, d, 64);
+    v = y < v ? y : v;
+  }
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) m = red[i] < m ? red[i] : m;
+  __syncthreads();
+  return m;
+}
+
+// ---- reference failure precedence (see tdb_oracle.c copy_in_out) ----------
+// FilterBuffer::write(FilterBuffer*, n) (filter_buffer.cc:393-424).
+__device__ __forceinline__ uint32_t copy_fail(uint64_t in_n, uint64_t ip,
+                                              uint64_t cap, uint64_t op,
+                                              uint64_t n) {
+  const uint64_t avail = ip < in_n ? in_n - ip : 0;
+  const uint64_t k = n < avail ? n : avail;
+  const uint64_t room = op < cap ? cap - op : 0;
+  if (k > 0 && room == 0) return TDBG_E_OUT_FULL;
+  if (k > room) return TDBG_E_OUT_FULL;
+  if (k < n) return TDBG_E_DATA_READ;
+  return 0;
+}
+
+// ne elements, each read cb bytes at ip + j*cb then write wb bytes at
+// op + j*wb; the read of element j precedes its write.
+__device__ __forceinline__ uint32_t elem_fail(uint64_t in_n, uint64_t ip,
+                                              uint32_t cb, uint64_t cap,
+                                              uint64_t op, uint32_t wb,
+                                              uint64_t ne) {
+  uint64_t jr = ne, jw = ne;
+  if (ip + ne * cb > in_n) jr = ip >= in_n ? 0 : (in_n - ip) / cb;
+  if (op + ne * wb > cap) jw = op >= cap ? 0 : (cap - op) / wb;
+  if (jr >= ne && jw >= ne) return 0;
+  return jr <= jw ? TDBG_E_DATA_READ : TDBG_E_OUT_FULL;
+}
+
+// DoubleDelta::decompress read/write sequence (dd_compressor.cc:314-404):
+// R v0, W v0, [num==1], R v1, W v1, [num==2], R word0, then per code i>=2
+// the word reads it triggers and W x_i.  Returns the first failure.
+__device__ __forceinline__ int dd_check(uint64_t cn, uint64_t un, uint32_t w,
+                                        uint32_t b, uint64_t num) {
+  const uint64_t NONE = ~0ull;
+  uint64_t rord = NONE, word = NONE;
+  const uint64_t nvals = num == 0 ? 2 : num;
+  // reads
+  if (cn < 9 + (uint64_t)w) rord = 0;
+  else if (num != 1) {
+    if (cn < 9 + 2ull * w) rord = 2;
+    else if (num != 2) {
+      const uint64_t base = 9 + 2ull * w;
+      const uint64_t A = (cn - base) / 8, rem = (cn - base) % 8;
+      if (A == 0) rord = 4;
+      else {
+        uint64_t ir = NONE;
+        if (b == 0) {
+          ir = 64 * A + 1;
+          if (ir < 2) ir = 2;
+        } else {
+          ir = 2 + (64 * A) / (b + 1);
+          if (rem > 0 && (64 * A) % (b + 1) == 0) {
+            const uint64_t ib = 1 + (64 * A) / (b + 1);
+            if (ib >= 2 && ib < ir) ir = ib;
+          }
+        }
+        if (ir < num) rord = 5 + 2 * (ir - 2);
+      }
+    }
+  }
+  // writes
+  const uint64_t iw = un / w;
+  if (iw < nvals) {
+    if (iw == 0) word = 1;
+    else if (iw == 1) word = 3;
+    else word = 6 + 2 * (iw - 2);
+  }
+  if (rord == NONE && word == NONE) return 0;
+  return rord <= word ? TDBG_E_DATA_READ : TDBG_E_OUT_FULL;
+}
+
+// Code of value i (j = i - 2) at bit s = j*(b+1) of the MSB-first u64 word
+// stream: sign bit then b magnitude bits (dd_compressor.cc:356-404).
+__device__ __forceinline__ uint64_t dd_code(const uint8_t* bs, uint64_t s, uint32_t b) {
+  const uint64_t wi = s >> 6;
+  const uint32_t r = (uint32_t)(s & 63);
+  uint64_t hi = ldn(bs + 8 * wi, 8) << r;
+  if (r + b + 1 > 64) hi |= ldn(bs + 8 * (wi + 1), 8) >> (64 - r);
+  const uint64_t code = hi >> (63 - b);
+  const uint64_t mag = b ? (code & ((1ull << b) - 1)) : 0;
+  return ((code >> b) & 1) ? (0 - mag) : mag;
+}
+
+// ---- double-delta second-order tuple scan ----------------------------------
+// For a run of n elements with first differences e: E = sum e,
+// X = sum_m sum_{k<=m} e_k.  Concatenating A then B (n_B elements):
+// E = E_A + E_B, X = X_A + X_B + n_B * E_A.
+struct DDAgg { uint64_t E, X; };
+struct DDCarry { uint64_t E, X; };
+
+__device__ __forceinline__ DDAgg dd_local(const uint64_t (&e)[DD_EPT]) {
+  DDAgg a = {0, 0};
+#pragma unroll
+  for (int k = 0; k < DD_EPT; k++) { a.E += e[k]; a.X += a.E; }
+  return a;
+}
+
+// Exclusive scan of DDAgg over the block (each thread = DD_EPT elements).
+// Writes the whole-round aggregate to `total`.
+template <int NT = GEN_NT>
+__device__ __forceinline__ DDAgg block_ddscan2(DDAgg a, DDAgg& total, uint64_t* red) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  DDAgg inc = a;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t oE = __shfl_up(inc.E, d, 64);
+    const uint64_t oX = __shfl_up(inc.X, d, 64);
+    if (lane >= (uint32_t)d) {
+      inc.X = oX + inc.X + (uint64_t)d * DD_EPT * oE;
+      inc.E = oE + inc.E;
+    }
+  }
+  DDAgg ex;
+  ex.E = __shfl_up(inc.E, 1, 64);
+  ex.X = __shfl_up(inc.X, 1, 64);
+  if (lane == 0) { ex.E = 0; ex.X = 0; }
+  if (lane == 63) { red[2 * wid] = inc.E; red[2 * wid + 1] = inc.X; }
+  __syncthreads();
+  DDAgg P = {0, 0}, T = {0, 0};
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const uint64_t wE = red[2 * i], wX = red[2 * i + 1];
+    if ((uint32_t)i < wid) { P.X = P.X + wX + 64ull * DD_EPT * P.E; P.E += wE; }
+    T.X = T.X + wX + 64ull * DD_EPT * T.E;
+    T.E += wE;
+  }
+  __syncthreads();
+  DDAgg r;
+  r.E = P.E + ex.E;
+  r.X = P.X + ex.X + (uint64_t)lane * DD_EPT * P.E;
+  total = T;
+  return r;
+}
+
+}  // namespace tdbg

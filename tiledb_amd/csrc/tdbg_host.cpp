@@ -1,0 +1,795 @@
+// tdbg_host.cpp -- host orchestration + C-ABI of the MI355X unfilter engine.
+//
+// Replaces, on the read path, ReaderBase::unfilter_tiles' CPU loop
+// (tiledb/sm/query/readers/reader_base.cc:905-989) over
+// FilterPipeline::run_reverse (filter_pipeline.cc:439-517).  The pipeline
+// descriptor is parsed exactly as FilterPipeline::deserialize
+// (filter_pipeline.cc:544-557) / FilterCreate::deserialize
+// (filter_create.cc:100-201), datatypes are chained as in
+// FilterPipeline(other, on_disk_type) (filter_pipeline.cc:80-88), and each
+// filter is resolved to a device stage kind with the widths the reference
+// picks at run time.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/tiledb_amd.h"
+#include "tdbg_desc.h"
+
+extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
+                                          hipStream_t stream);
+extern "C" hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid,
+                                       hipStream_t stream);
+extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan);
+extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess)                                                   \
+      return fail(TDBG_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- datatypes (tiledb/sm/enums/datatype.h:67-140) -------------------------
+uint32_t dt_size(uint8_t dt) {
+  switch (dt) {
+    case TDBG_INT32: case TDBG_FLOAT32: case TDBG_UINT32:
+    case TDBG_STRING_UTF32: case TDBG_STRING_UCS4:
+      return 4;
+    case TDBG_INT64: case TDBG_FLOAT64: case TDBG_UINT64:
+      return 8;
+    case TDBG_INT16: case TDBG_UINT16: case TDBG_STRING_UTF16: case TDBG_STRING_UCS2:
+      return 2;
+    default:
+      return (dt >= 18 && dt <= 39) ? 8 : 1;
+  }
+}
+bool is_dt_time(uint8_t dt) { return dt >= 18 && dt <= 39; }
+
+struct Filter {
+  uint8_t type = 0;
+  uint8_t compressor = 0;
+  int32_t level = 0;
+  uint8_t reinterpret = TDBG_ANY;
+  uint32_t window = 0;
+  uint8_t datatype = 0;
+};
+
+uint8_t compressor_filter(uint8_t c) {
+  static const uint8_t m[] = {TDBG_FILTER_NONE, TDBG_FILTER_GZIP, TDBG_FILTER_ZSTD,
+                              TDBG_FILTER_LZ4, TDBG_FILTER_RLE, TDBG_FILTER_BZIP2,
+                              TDBG_FILTER_DOUBLE_DELTA, TDBG_FILTER_DICTIONARY,
+                              TDBG_FILTER_DELTA};
+  return c < sizeof(m) ? m[c] : 0xff;
+}
+
+}  // namespace
+
+struct tdbg_pipeline {
+  uint32_t max_chunk_size = 0;
+  uint32_t version = 0;
+  uint8_t on_disk_type = 0;
+  uint64_t cell_size = 0;
+  std::vector<Filter> filters;
+  tdbg_plan plan{};
+  bool supported = true;
+};
+
+struct tdbg_context {
+  int device = 0;
+  int cus = 256;
+  // general-path scratch
+  uint8_t* scratch = nullptr;
+  uint64_t scratch_bytes = 0;
+  uint32_t slot_cap = 80 * 1024, md_cap = 16 * 1024, tab_cap = 32 * 1024;
+  // per-tile status / need
+  int32_t* d_status = nullptr;
+  uint64_t* d_need = nullptr;
+  uint64_t status_cap = 0;
+  uint32_t* d_list = nullptr;
+  uint64_t list_cap = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  uint64_t tiles_unfiltered = 0, bytes_unfiltered = 0;
+  // host E2E staging
+  struct Stage {
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint64_t in_cap = 0, out_cap = 0;
+    const uint8_t** h_ptrs = nullptr;  // pinned: in ptrs, sizes, out ptrs, sizes
+    uint64_t ptr_cap = 0;
+    void* d_ptrs = nullptr;
+    int32_t* h_status = nullptr;
+    int32_t* d_stat = nullptr;
+    hipStream_t stream = nullptr;  // copy stream of this slot
+    hipEvent_t h2d = nullptr, kdone = nullptr, done = nullptr;
+  } st[2];
+  hipStream_t cstream = nullptr;   // compute stream: kernels serialized (shared scratch)
+};
+
+namespace {
+
+uint64_t slot_bytes(const tdbg_context* c) {
+  return 2ull * c->slot_cap + 2ull * c->md_cap + c->tab_cap;
+}
+
+int ensure_scratch(tdbg_context* c, uint32_t grid) {
+  const uint64_t need = slot_bytes(c) * grid;
+  if (need <= c->scratch_bytes) return TDBG_OK;
+  if (c->scratch) HIP_OK(hipFree(c->scratch));
+  c->scratch = nullptr;
+  HIP_OK(hipMalloc(&c->scratch, need));
+  c->scratch_bytes = need;
+  return TDBG_OK;
+}
+
+int ensure_status(tdbg_context* c, uint64_t n) {
+  if (n <= c->status_cap) return TDBG_OK;
+  if (c->d_status) HIP_OK(hipFree(c->d_status));
+  if (c->d_need) HIP_OK(hipFree(c->d_need));
+  HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
+  HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
+  c->status_cap = n;
+  return TDBG_OK;
+}
+
+// Resolve filters to device stages (the run-time datatype switches of the
+// reference): bit_width_reduction_filter.cc:288-350,
+// positive_delta_filter.cc:262-322, dd_compressor.cc:131-200,
+// compression_filter.cc:303-486.
+void build_plan(tdbg_pipeline* p) {
+  tdbg_plan& P = p->plan;
+  memset(&P, 0, sizeof(P));
+  P.nstages = (uint32_t)p->filters.size();
+  p->supported = P.nstages <= TDBG_MAX_FILTERS;
+  for (uint32_t i = 0; i < P.nstages && i < TDBG_MAX_FILTERS; i++) {
+    const Filter& f = p->filters[i];
+    tdbg_stage& s = P.s[i];
+    const uint8_t dt = f.datatype;
+    s.dts = (uint8_t)dt_size(dt);
+    switch (f.type) {
+      case TDBG_FILTER_NONE:
+        s.kind = TDBG_K_PASS;
+        break;
+      case TDBG_FILTER_BYTESHUFFLE:
+        s.kind = TDBG_K_BYTESHUFFLE;
+        s.w = (uint8_t)dt_size(dt);
+        break;
+      case TDBG_FILTER_BITSHUFFLE:
+        s.kind = TDBG_K_BITSHUFFLE;
+        s.w = (uint8_t)dt_size(dt);
+        break;
+      case TDBG_FILTER_BIT_WIDTH_REDUCTION:
+      case TDBG_FILTER_POSITIVE_DELTA: {
+        const bool bwr = f.type == TDBG_FILTER_BIT_WIDTH_REDUCTION;
+        int w = 0, sg = 0;
+        switch (dt) {
+          case TDBG_INT16: w = 2; sg = 1; break;
+          case TDBG_UINT16: w = 2; break;
+          case TDBG_INT32: w = 4; sg = 1; break;
+          case TDBG_UINT32: w = 4; break;
+          case TDBG_INT64: w = 8; sg = 1; break;
+          case TDBG_UINT64: w = 8; break;
+          case TDBG_INT8: if (!bwr) { w = 1; sg = 1; } break;
+          case TDBG_UINT8: case TDBG_BLOB: case TDBG_GEOM_WKB: case TDBG_GEOM_WKT:
+          case TDBG_BOOL: if (!bwr) w = 1; break;
+          default:
+            if (is_dt_time(dt) && p->version >= 20) { w = 8; sg = 1; }
+        }
+        if (w == 0) { s.kind = TDBG_K_PASS; break; }
+        s.kind = bwr ? TDBG_K_BWR : TDBG_K_PD;
+        s.w = (uint8_t)w;
+        s.sgn = (uint8_t)sg;
+        s.window = f.window;
+        break;
+      }
+      case TDBG_FILTER_DOUBLE_DELTA: case TDBG_FILTER_RLE: case TDBG_FILTER_GZIP:
+      case TDBG_FILTER_ZSTD: case TDBG_FILTER_LZ4: case TDBG_FILTER_BZIP2:
+      case TDBG_FILTER_DICTIONARY: case TDBG_FILTER_DELTA:
+        if (f.compressor == TDBG_COMPRESSOR_NONE) {
+          s.kind = TDBG_K_PASS;
+        } else if (f.compressor == TDBG_COMPRESSOR_RLE) {
+          if ((dt == TDBG_STRING_ASCII || dt == TDBG_STRING_UTF8) && p->version >= 12) {
+            // var-string RLE (compression_filter.cc:331-338) is only taken
+            // with an offsets tile; fixed-size RLE otherwise.  Still fixed.
+          }
+          s.kind = TDBG_K_RLE;
+          s.cs = p->cell_size;
+          if (p->cell_size == 0) { s.kind = TDBG_K_UNSUPPORTED; p->supported = false; }
+        } else if (f.compressor == TDBG_COMPRESSOR_DOUBLE_DELTA) {
+          s.kind = TDBG_K_DD;
+          const uint8_t t = f.reinterpret != TDBG_ANY ? f.reinterpret : dt;
+          switch (t) {
+            case TDBG_FLOAT32: case TDBG_FLOAT64: s.w = 0; break;  // DD_TYPE at run time
+            default: s.w = (uint8_t)(t <= 43 ? dt_size(t) : 0);
+          }
+          if (t == TDBG_STRING_ASCII || t == TDBG_STRING_UTF8 || t == TDBG_STRING_UTF16 ||
+              t == TDBG_STRING_UTF32 || t == TDBG_STRING_UCS2 || t == TDBG_STRING_UCS4 ||
+              t == TDBG_ANY)
+            s.w = 1;  // DoubleDelta::decompress<uint8_t> (dd_compressor.cc:187-194)
+        } else {
+          s.kind = TDBG_K_UNSUPPORTED;
+          p->supported = false;
+        }
+        break;
+      default:
+        s.kind = TDBG_K_UNSUPPORTED;
+        p->supported = false;
+    }
+  }
+  P.fast = p->supported ? tdbg_fast_select(&P) : 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+size_t tdbg_last_error(char* buf, size_t cap) {
+  if (!buf || cap == 0) return g_err.size();
+  const size_t n = std::min(cap - 1, g_err.size());
+  memcpy(buf, g_err.data(), n);
+  buf[n] = 0;
+  return n;
+}
+
+const char* tdbg_status_str(int s) {
+  switch (s) {
+    case TDBG_OK: return "ok";
+    case TDBG_E_ARG: return "invalid argument";
+    case TDBG_E_TILE_FORMAT: return "Tile chunk directory exceeds the filtered tile";
+    case TDBG_E_TILE_SIZE: return "Incorrect unfiltered tile size allocated.";
+    case TDBG_E_MD_READ: return "FilterBuffer error; could not read requested byte count.";
+    case TDBG_E_DATA_READ: return "Filter input too short for its metadata";
+    case TDBG_E_OUT_FULL: return "FilterBuffer error; could not write: buffer is full.";
+    case TDBG_E_RLE_FORMAT: return "Failed decompressing with RLE; invalid input buffer format";
+    case TDBG_E_DD_TYPE: return "DoubleDelta tile decompression is not yet supported for float types.";
+    case TDBG_E_BWR_BITS: return "Bit width reduction: invalid compressed bit width";
+    case TDBG_E_UNSUPPORTED: return "Filter not supported by the MI355X engine";
+    case TDBG_E_SCRATCH: return "internal: scratch too small";
+    case TDBG_E_PD_DECREASING: return "Positive delta filter error: delta is not positive.";
+    case TDBG_E_DD_OVERFLOW: return "Cannot compress with DoubleDelta: delta exceeds range of int64_t";
+    case TDBG_E_DEVICE: return "HIP runtime error";
+    case TDBG_E_DESCRIPTOR: return "Deserialization error; malformed filter pipeline";
+    default: return "unknown";
+  }
+}
+
+int tdbg_pipeline_create(const uint8_t* b, size_t len, uint32_t version,
+                         uint8_t datatype, uint64_t cell_size, tdbg_pipeline** out) {
+  if (!b || !out) return fail(TDBG_E_ARG, "tdbg_pipeline_create: null argument");
+  auto p = new tdbg_pipeline();
+  size_t o = 0;
+  auto need = [&](size_t k) { return o + k <= len; };
+  auto rd32 = [&](size_t at) { uint32_t v; memcpy(&v, b + at, 4); return v; };
+  if (!need(8)) { delete p; return fail(TDBG_E_DESCRIPTOR, "pipeline descriptor shorter than 8 bytes"); }
+  p->max_chunk_size = rd32(0);
+  const uint32_t nf = rd32(4);
+  o = 8;
+  p->version = version;
+  p->on_disk_type = datatype;
+  p->cell_size = cell_size;
+  uint8_t cur = datatype;
+  for (uint32_t i = 0; i < nf; i++) {
+    if (!need(5)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated filter header"); }
+    Filter f;
+    f.type = b[o];
+    const uint32_t mdlen = rd32(o + 1);
+    o += 5;
+    if (len - o < mdlen) {
+      delete p;
+      return fail(TDBG_E_DESCRIPTOR, "Deserialization error; not enough data in buffer for metadata");
+    }
+    switch (f.type) {
+      case TDBG_FILTER_NONE: break;
+      case TDBG_FILTER_GZIP: case TDBG_FILTER_ZSTD: case TDBG_FILTER_LZ4: case TDBG_FILTER_RLE:
+      case TDBG_FILTER_BZIP2: case TDBG_FILTER_DELTA: case TDBG_FILTER_DOUBLE_DELTA:
+      case TDBG_FILTER_DICTIONARY: {
+        if (!need(5)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated compressor options"); }
+        const uint8_t ftype = f.type;
+        f.compressor = b[o];
+        memcpy(&f.level, b + o + 1, 4);
+        o += 5;
+        if ((version >= 20 && ftype == TDBG_FILTER_DOUBLE_DELTA) ||
+            (version >= 19 && ftype == TDBG_FILTER_DELTA)) {
+          if (!need(1)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated reinterpret type"); }
+          f.reinterpret = b[o++];
+        }
+        f.type = compressor_filter(f.compressor);
+        if (f.type == 0xff) { delete p; return fail(TDBG_E_DESCRIPTOR, "unknown compressor"); }
+        break;
+      }
+      case TDBG_FILTER_BIT_WIDTH_REDUCTION: case TDBG_FILTER_POSITIVE_DELTA:
+        if (!need(4)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated window option"); }
+        f.window = rd32(o);
+        o += 4;
+        break;
+      case TDBG_FILTER_BITSHUFFLE: case TDBG_FILTER_BYTESHUFFLE: case TDBG_FILTER_AES_256_GCM:
+      case TDBG_FILTER_CHECKSUM_MD5: case TDBG_FILTER_CHECKSUM_SHA256: case TDBG_FILTER_XOR:
+        break;
+      case TDBG_FILTER_SCALE_FLOAT:
+        if (!need(24)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated float scale config"); }
+        o += 24;
+        break;
+      case TDBG_FILTER_WEBP:
+        o += mdlen;
+        break;
+      default:
+        delete p;
+        return fail(TDBG_E_DESCRIPTOR, "Deserialization error; unknown type");
+    }
+    f.datatype = cur;
+    if ((f.type == TDBG_FILTER_DOUBLE_DELTA || f.type == TDBG_FILTER_DELTA) &&
+        f.reinterpret != TDBG_ANY)
+      cur = f.reinterpret;  // CompressionFilter::output_datatype
+    p->filters.push_back(f);
+  }
+  build_plan(p);
+  *out = p;
+  return TDBG_OK;
+}
+
+void tdbg_pipeline_destroy(tdbg_pipeline* p) { delete p; }
+int tdbg_pipeline_supported(const tdbg_pipeline* p) { return p && p->supported ? 1 : 0; }
+uint32_t tdbg_pipeline_num_filters(const tdbg_pipeline* p) {
+  return p ? (uint32_t)p->filters.size() : 0;
+}
+int tdbg_pipeline_filter(const tdbg_pipeline* p, uint32_t i, uint8_t* type, uint8_t* dt) {
+  if (!p || i >= p->filters.size()) return fail(TDBG_E_ARG, "filter index out of range");
+  if (type) *type = p->filters[i].type;
+  if (dt) *dt = p->filters[i].datatype;
+  return TDBG_OK;
+}
+
+int tdbg_context_create(int device, tdbg_context** out) {
+  if (!out) return fail(TDBG_E_ARG, "null out");
+  HIP_OK(hipSetDevice(device));
+  auto c = new tdbg_context();
+  c->device = device;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    c->cus = cus;
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return fail(TDBG_E_DEVICE, "hipEventCreate failed");
+  }
+  *out = c;
+  return TDBG_OK;
+}
+
+void tdbg_context_destroy(tdbg_context* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->d_status) (void)hipFree(c->d_status);
+  if (c->d_need) (void)hipFree(c->d_need);
+  if (c->d_list) (void)hipFree(c->d_list);
+  for (auto& s : c->st) {
+    if (s.d_in) (void)hipFree(s.d_in);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.d_ptrs) (void)hipFree(s.d_ptrs);
+    if (s.h_ptrs) (void)hipHostFree(s.h_ptrs);
+    if (s.h_status) (void)hipHostFree(s.h_status);
+    if (s.d_stat) (void)hipFree(s.d_stat);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.h2d) (void)hipEventDestroy(s.h2d);
+    if (s.kdone) (void)hipEventDestroy(s.kdone);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                  const uint8_t* const* d_in, const uint64_t* d_in_size,
+                  uint8_t* const* d_out, const uint64_t* d_out_size, uint32_t flags,
+                  int32_t* d_status, uint64_t* d_need, const uint32_t* d_list,
+                  hipStream_t stream, bool force_general) {
+  if (ntiles == 0) return TDBG_OK;
+  tdbg::KParams kp{};
+  kp.in = d_in;
+  kp.in_size = d_in_size;
+  kp.out = d_out;
+  kp.out_size = d_out_size;
+  kp.status = d_status;
+  kp.need = d_need;
+  kp.tile_list = d_list;
+  kp.ntiles = ntiles;
+  kp.flags = flags;
+  kp.plan = p->plan;
+  const bool fast = !force_general && p->plan.fast != 0;
+  uint32_t grid;
+  if (fast) {
+    grid = tdbg_fast_grid(p->plan.fast, c->cus);
+  } else {
+    grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
+  }
+  // The fast kernels fall back to the general interpreter per chunk, so both
+  // need the scratch slots.
+  int rc = ensure_scratch(c, grid);
+  if (rc) return rc;
+  kp.scratch = c->scratch;
+  kp.slot_bytes = slot_bytes(c);
+  kp.slot_cap = c->slot_cap;
+  kp.md_cap = c->md_cap;
+  kp.tab_cap = c->tab_cap;
+  HIP_OK(hipEventRecord(c->ev0, stream));
+  hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  HIP_OK(hipEventRecord(c->ev1, stream));
+  c->timed = true;
+  return TDBG_OK;
+}
+
+int tdbg_unfilter_tiles_async(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                              const uint8_t* const* d_in, const uint64_t* d_in_size,
+                              uint8_t* const* d_out, const uint64_t* d_out_size,
+                              uint32_t flags, int32_t* d_status, tdbg_stream stream) {
+  if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (ntiles && (!d_in || !d_in_size || !d_out || !d_out_size))
+    return fail(TDBG_E_ARG, "null tile arrays");
+  if (ntiles > 0xffffffffull) return fail(TDBG_E_ARG, "too many tiles in one call");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = ensure_status(c, ntiles);
+  if (rc) return rc;
+  rc = launch(c, p, ntiles, d_in, d_in_size, d_out, d_out_size, flags,
+              d_status ? d_status : c->d_status, c->d_need, nullptr, (hipStream_t)stream, false);
+  if (rc) return rc;
+  c->tiles_unfiltered += ntiles;
+  return TDBG_OK;
+}
+
+int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                             const uint8_t* const* d_in, const uint64_t* d_in_size,
+                             uint8_t* const* d_out, const uint64_t* d_out_size,
+                             uint32_t flags, int32_t* host_status, tdbg_stream stream) {
+  if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (ntiles == 0) return TDBG_OK;
+  if (!d_in || !d_in_size || !d_out || !d_out_size) return fail(TDBG_E_ARG, "null tile arrays");
+  if (ntiles > 0xffffffffull) return fail(TDBG_E_ARG, "too many tiles in one call");
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_status(c, ntiles);
+  if (rc) return rc;
+  rc = launch(c, p, ntiles, d_in, d_in_size, d_out, d_out_size, flags, c->d_status, c->d_need,
+              nullptr, s, false);
+  if (rc) return rc;
+  std::vector<int32_t> st(ntiles);
+  std::vector<uint64_t> need(ntiles);
+  HIP_OK(hipMemcpyAsync(st.data(), c->d_status, ntiles * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(need.data(), c->d_need, ntiles * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  // Resolve TDBG_E_SCRATCH tiles with the general interpreter and bigger
+  // scratch slots; each pass discovers one more stage's size.
+  for (int pass = 0; pass < 2 * TDBG_MAX_FILTERS + 2; pass++) {
+    std::vector<uint32_t> list;
+    uint64_t maxneed = 0;
+    for (uint64_t i = 0; i < ntiles; i++)
+      if (st[i] == TDBG_E_SCRATCH) { list.push_back((uint32_t)i); maxneed = std::max(maxneed, need[i]); }
+    if (list.empty()) break;
+    const uint64_t grow = std::max<uint64_t>(maxneed + maxneed / 4 + 256, 0);
+    if (grow > 0xffffffffull / 2) return fail(TDBG_E_SCRATCH, "chunk stage larger than 2 GiB");
+    c->slot_cap = (uint32_t)std::max<uint64_t>(c->slot_cap, (grow + 255) & ~255ull);
+    c->md_cap = (uint32_t)std::max<uint64_t>(c->md_cap, (grow + 255) & ~255ull);
+    c->tab_cap = (uint32_t)std::max<uint64_t>(c->tab_cap, (grow + 255) & ~255ull);
+    if (list.size() > c->list_cap) {
+      if (c->d_list) HIP_OK(hipFree(c->d_list));
+      HIP_OK(hipMalloc(&c->d_list, list.size() * 4));
+      c->list_cap = list.size();
+    }
+    HIP_OK(hipMemcpyAsync(c->d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(list.size(), 256);
+    // shrink scratch for the retry: fewer, bigger slots
+    if (c->scratch && slot_bytes(c) * grid > c->scratch_bytes) {
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipFree(c->scratch));
+      c->scratch = nullptr;
+      c->scratch_bytes = 0;
+    }
+    rc = ensure_scratch(c, grid);
+    if (rc) return rc;
+    tdbg::KParams kp{};
+    kp.in = d_in; kp.in_size = d_in_size; kp.out = d_out; kp.out_size = d_out_size;
+    kp.status = c->d_status; kp.need = c->d_need; kp.tile_list = c->d_list;
+    kp.ntiles = list.size(); kp.flags = flags; kp.plan = p->plan;
+    kp.scratch = c->scratch; kp.slot_bytes = slot_bytes(c);
+    kp.slot_cap = c->slot_cap; kp.md_cap = c->md_cap; kp.tab_cap = c->tab_cap;
+    hipError_t e = tdbg_launch_general(&kp, grid, s);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("retry launch: ") + hipGetErrorString(e));
+    HIP_OK(hipMemcpyAsync(st.data(), c->d_status, ntiles * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(need.data(), c->d_need, ntiles * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  if (host_status) memcpy(host_status, st.data(), ntiles * 4);
+  c->tiles_unfiltered += ntiles;
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (st[i]) {
+      char msg[160];
+      snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
+      return fail(st[i], msg);
+    }
+  return TDBG_OK;
+}
+
+int tdbg_context_stats(const tdbg_context* c, uint64_t* tiles, uint64_t* bytes) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (tiles) *tiles = c->tiles_unfiltered;
+  if (bytes) *bytes = c->bytes_unfiltered;
+  return TDBG_OK;
+}
+
+int tdbg_context_last_kernel_ms(tdbg_context* c, float* ms) {
+  if (!c || !ms) return fail(TDBG_E_ARG, "null argument");
+  if (!c->timed) return fail(TDBG_E_ARG, "no kernel launched yet");
+  HIP_OK(hipEventSynchronize(c->ev1));
+  HIP_OK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return TDBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host-resident end-to-end
+// ---------------------------------------------------------------------------
+static int stage_reserve(tdbg_context::Stage& s, uint64_t in_b, uint64_t out_b, uint64_t nt) {
+  if (!s.stream) {
+    HIP_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  }
+  if (in_b > s.in_cap) {
+    if (s.d_in) HIP_OK(hipFree(s.d_in));
+    HIP_OK(hipMalloc(&s.d_in, in_b));
+    s.in_cap = in_b;
+  }
+  if (out_b > s.out_cap) {
+    if (s.d_out) HIP_OK(hipFree(s.d_out));
+    HIP_OK(hipMalloc(&s.d_out, out_b));
+    s.out_cap = out_b;
+  }
+  if (nt > s.ptr_cap) {
+    if (s.d_ptrs) HIP_OK(hipFree(s.d_ptrs));
+    if (s.h_ptrs) HIP_OK(hipHostFree(s.h_ptrs));
+    if (s.h_status) HIP_OK(hipHostFree(s.h_status));
+    if (s.d_stat) HIP_OK(hipFree(s.d_stat));
+    HIP_OK(hipMalloc(&s.d_stat, nt * 4));
+    HIP_OK(hipMalloc(&s.d_ptrs, nt * 32));
+    HIP_OK(hipHostMalloc((void**)&s.h_ptrs, nt * 32));
+    HIP_OK(hipHostMalloc((void**)&s.h_status, nt * 4));
+    s.ptr_cap = nt;
+  }
+  return TDBG_OK;
+}
+
+// Coalesced copies: consecutive tiles contiguous in host memory move as one
+// hipMemcpyAsync.
+static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* const* host,
+                       const uint64_t* size, uint8_t* dev_base, bool h2d,
+                       uint8_t* const* host_out) {
+  uint64_t i = lo;
+  uint64_t doff = 0;
+  while (i < hi) {
+    uint64_t j = i + 1;
+    uint64_t bytes = size[i];
+    if (h2d) {
+      while (j < hi && host[j] == host[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
+      if (bytes) HIP_OK(hipMemcpyAsync(dev_base + doff, host[i], bytes, hipMemcpyHostToDevice, st));
+    } else {
+      while (j < hi && host_out[j] == host_out[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
+      if (bytes) HIP_OK(hipMemcpyAsync(host_out[i], dev_base + doff, bytes, hipMemcpyDeviceToHost, st));
+    }
+    doff += bytes;
+    i = j;
+  }
+  return TDBG_OK;
+}
+
+int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                             const uint8_t* const* in, const uint64_t* in_size,
+                             uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
+                             int32_t* host_status, uint64_t batch_bytes) {
+  if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (ntiles == 0) return TDBG_OK;
+  if (!in || !in_size || !out || !out_size) return fail(TDBG_E_ARG, "null tile arrays");
+  HIP_OK(hipSetDevice(c->device));
+  if (batch_bytes == 0) batch_bytes = 256ull << 20;
+  if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  // batches bounded by bytes on both sides
+  std::vector<uint64_t> cuts{0};
+  uint64_t bi = 0, bo = 0;
+  for (uint64_t i = 0; i < ntiles; i++) {
+    if (i > cuts.back() && (bi + in_size[i] > batch_bytes || bo + out_size[i] > batch_bytes)) {
+      cuts.push_back(i);
+      bi = bo = 0;
+    }
+    bi += in_size[i];
+    bo += out_size[i];
+  }
+  cuts.push_back(ntiles);
+  std::vector<int32_t> st(ntiles, 0);
+  const size_t nb = cuts.size() - 1;
+  std::vector<bool> pending(2, false);
+  std::vector<uint64_t> plo(2), phi(2);
+  auto collect = [&](int k) -> int {
+    auto& S = c->st[k];
+    HIP_OK(hipEventSynchronize(S.done));
+    memcpy(st.data() + plo[k], S.h_status, (phi[k] - plo[k]) * 4);
+    pending[k] = false;
+    return TDBG_OK;
+  };
+  for (size_t b = 0; b < nb; b++) {
+    const int k = (int)(b & 1);
+    auto& S = c->st[k];
+    if (pending[k]) { int rc = collect(k); if (rc) return rc; }
+    const uint64_t lo = cuts[b], hi = cuts[b + 1], nt = hi - lo;
+    uint64_t ib = 0, ob = 0;
+    for (uint64_t i = lo; i < hi; i++) { ib += in_size[i]; ob += out_size[i]; }
+    int rc = stage_reserve(S, ib + 16, ob + 16, nt);
+    if (rc) return rc;
+    // pointer/size arrays (pinned) -> device
+    const uint8_t** hp = S.h_ptrs;
+    uint64_t* hs = (uint64_t*)(hp + nt);
+    uint8_t** ho = (uint8_t**)(hs + nt);
+    uint64_t* hos = (uint64_t*)(ho + nt);
+    uint64_t io = 0, oo = 0;
+    for (uint64_t i = lo; i < hi; i++) {
+      hp[i - lo] = S.d_in + io;
+      hs[i - lo] = in_size[i];
+      ho[i - lo] = S.d_out + oo;
+      hos[i - lo] = out_size[i];
+      io += in_size[i];
+      oo += out_size[i];
+    }
+    HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, S.stream));
+    rc = copy_ranges(S.stream, lo, hi, in, in_size, S.d_in, true, nullptr);
+    if (rc) return rc;
+    const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
+    const uint64_t* ds = (const uint64_t*)(dp + nt);
+    uint8_t* const* dop = (uint8_t* const*)(ds + nt);
+    const uint64_t* dos = (const uint64_t*)(dop + nt);
+    HIP_OK(hipEventRecord(S.h2d, S.stream));
+    // kernels serialize on the compute stream (they share the scratch slots)
+    HIP_OK(hipStreamWaitEvent(c->cstream, S.h2d, 0));
+    rc = ensure_status(c, nt);
+    if (rc) return rc;
+    rc = launch(c, p, nt, dp, ds, dop, dos, flags, S.d_stat, c->d_need, nullptr, c->cstream, false);
+    if (rc) return rc;
+    HIP_OK(hipEventRecord(S.kdone, c->cstream));
+    HIP_OK(hipStreamWaitEvent(S.stream, S.kdone, 0));
+    HIP_OK(hipMemcpyAsync(S.h_status, S.d_stat, nt * 4, hipMemcpyDeviceToHost, S.stream));
+    rc = copy_ranges(S.stream, lo, hi, nullptr, out_size, S.d_out, false, out);
+    if (rc) return rc;
+    HIP_OK(hipEventRecord(S.done, S.stream));
+    pending[k] = true;
+    plo[k] = lo;
+    phi[k] = hi;
+  }
+  for (int k = 0; k < 2; k++)
+    if (pending[k]) { int rc = collect(k); if (rc) return rc; }
+  c->tiles_unfiltered += ntiles;
+  // tiles that needed bigger scratch: redo them one by one through the sync path
+  for (uint64_t i = 0; i < ntiles; i++) {
+    if (st[i] != TDBG_E_SCRATCH) continue;
+    auto& S = c->st[0];
+    int rc = stage_reserve(S, in_size[i] + 16, out_size[i] + 16, 1);
+    if (rc) return rc;
+    HIP_OK(hipMemcpy(S.d_in, in[i], in_size[i], hipMemcpyHostToDevice));
+    const uint8_t* hp[4] = {S.d_in, (const uint8_t*)in_size[i], S.d_out, (const uint8_t*)out_size[i]};
+    HIP_OK(hipMemcpy(S.d_ptrs, hp, 32, hipMemcpyHostToDevice));
+    const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
+    int32_t one = 0;
+    rc = tdbg_unfilter_tiles_sync(c, p, 1, dp, (const uint64_t*)(dp + 1), (uint8_t* const*)(dp + 2),
+                                  (const uint64_t*)(dp + 3), flags, &one, S.stream);
+    st[i] = one;
+    if (one == TDBG_OK) HIP_OK(hipMemcpy(out[i], S.d_out, out_size[i], hipMemcpyDeviceToHost));
+  }
+  if (host_status) memcpy(host_status, st.data(), ntiles * 4);
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (st[i]) {
+      char msg[160];
+      snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
+      return fail(st[i], msg);
+    }
+  return TDBG_OK;
+}
+
+int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
+                                  const uint8_t* const* in, const uint64_t* in_size,
+                                  uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
+                                  int32_t* host_status, const int* devices, int ndev,
+                                  uint64_t batch_bytes) {
+  if (!p || !devices || ndev <= 0) return fail(TDBG_E_ARG, "bad device list");
+  if (ntiles == 0) return TDBG_OK;
+  // contiguous shards balanced by filtered + unfiltered bytes
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < ntiles; i++) total += in_size[i] + out_size[i];
+  std::vector<uint64_t> cut{0};
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < ntiles && (int)cut.size() < ndev; i++) {
+    acc += in_size[i] + out_size[i];
+    if (acc * ndev >= total * cut.size()) cut.push_back(i + 1);
+  }
+  while ((int)cut.size() <= ndev) cut.push_back(ntiles);
+  cut[ndev] = ntiles;
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::string> errs(ndev);
+  std::vector<int32_t> st(ntiles, 0);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; d++) {
+    th.emplace_back([&, d]() {
+      const uint64_t lo = cut[d], hi = cut[d + 1];
+      if (hi <= lo) return;
+      tdbg_context* c = nullptr;
+      int rc = tdbg_context_create(devices[d], &c);
+      if (rc == TDBG_OK) {
+        rc = tdbg_unfilter_tiles_host(c, p, hi - lo, in + lo, in_size + lo, out + lo, out_size + lo,
+                                      flags, st.data() + lo, batch_bytes);
+        tdbg_context_destroy(c);
+      }
+      rcs[d] = rc;
+      if (rc) errs[d] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  if (host_status) memcpy(host_status, st.data(), ntiles * 4);
+  for (int d = 0; d < ndev; d++)
+    if (rcs[d] && rcs[d] != TDBG_OK) {
+      // report the first failing tile in tile order when it is a tile status
+      for (uint64_t i = 0; i < ntiles; i++)
+        if (st[i]) {
+          char msg[160];
+          snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
+          return fail(st[i], msg);
+        }
+      return fail(rcs[d], errs[d]);
+    }
+  return TDBG_OK;
+}
+
+int tdbg_device_alloc(int device, uint64_t bytes, void** out) {
+  if (!out) return fail(TDBG_E_ARG, "null out");
+  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipMalloc(out, bytes ? bytes : 1));
+  return TDBG_OK;
+}
+int tdbg_device_free(void* p) {
+  HIP_OK(hipFree(p));
+  return TDBG_OK;
+}
+int tdbg_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+  HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return TDBG_OK;
+}
+int tdbg_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+  HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return TDBG_OK;
+}
+int tdbg_device_count(int* n) {
+  if (!n) return fail(TDBG_E_ARG, "null out");
+  HIP_OK(hipGetDeviceCount(n));
+  return TDBG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,229 @@
+"""Python handles over the C-ABI: device pipelines, contexts, tile batches.
+
+PyTorch is used only as plumbing: device allocations (torch.uint8 tensors on
+cuda:N), the current HIP stream, and pinned host memory.  All unfilter work is
+done by libtiledb_amd.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import lib
+
+TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _check(rc: int, what: str) -> None:
+    if rc:
+        raise EngineError(rc, f"{what}: {_native.last_error() or _native.status_str(rc)}")
+
+
+class DevicePipeline:
+    """tdbg_pipeline: a parsed, immutable FilterPipeline descriptor."""
+
+    def __init__(self, serialized: bytes, version: int, on_disk_type: int, cell_size: int):
+        buf = (ctypes.c_uint8 * len(serialized)).from_buffer_copy(serialized)
+        h = ctypes.c_void_p()
+        _check(lib.tdbg_pipeline_create(buf, len(serialized), version, on_disk_type, cell_size,
+                                        ctypes.byref(h)), "tdbg_pipeline_create")
+        self.h = h
+        self.serialized = bytes(serialized)
+        self.version = version
+        self.on_disk_type = on_disk_type
+        self.cell_size = cell_size
+
+    @property
+    def supported(self) -> bool:
+        return bool(lib.tdbg_pipeline_supported(self.h))
+
+    @property
+    def num_filters(self) -> int:
+        return int(lib.tdbg_pipeline_num_filters(self.h))
+
+    def filter_info(self, i: int):
+        t = ctypes.c_uint8()
+        d = ctypes.c_uint8()
+        _check(lib.tdbg_pipeline_filter(self.h, i, ctypes.byref(t), ctypes.byref(d)),
+               "tdbg_pipeline_filter")
+        return int(t.value), int(d.value)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            lib.tdbg_pipeline_destroy(h)
+            self.h = None
+
+
+class TileBatch:
+    """Device-resident batch of filtered tiles and their output buffers.
+
+    Filtered tiles are packed back to back in `d_in` (uint8, device), outputs
+    in `d_out`; the per-tile device pointer / size arrays the C-ABI takes are
+    built once.
+    """
+
+    def __init__(self, d_in, in_off: np.ndarray, in_size: np.ndarray, d_out,
+                 out_off: np.ndarray, out_size: np.ndarray):
+        import torch
+        self.d_in, self.d_out = d_in, d_out
+        self.in_off = np.asarray(in_off, dtype=np.uint64)
+        self.in_size = np.asarray(in_size, dtype=np.uint64)
+        self.out_off = np.asarray(out_off, dtype=np.uint64)
+        self.out_size = np.asarray(out_size, dtype=np.uint64)
+        dev = d_in.device
+        ib, ob = d_in.data_ptr(), d_out.data_ptr()
+        meta = np.empty((4, self.ntiles), dtype=np.uint64)
+        meta[0] = self.in_off + np.uint64(ib)
+        meta[1] = self.in_size
+        meta[2] = self.out_off + np.uint64(ob)
+        meta[3] = self.out_size
+        self.d_meta = torch.from_numpy(meta.view(np.int64)).to(dev)
+        self.d_status = torch.zeros(max(self.ntiles, 1), dtype=torch.int32, device=dev)
+
+    @property
+    def ntiles(self) -> int:
+        return int(self.in_off.size)
+
+    def ptrs(self):
+        base = self.d_meta.data_ptr()
+        n = self.ntiles * 8
+        return base, base + n, base + 2 * n, base + 3 * n
+
+    @classmethod
+    def from_packed(cls, packed: np.ndarray, in_off, in_size, out_sizes, device: int = 0,
+                    fill: int = 0) -> "TileBatch":
+        import torch
+        dev = torch.device("cuda", device)
+        packed = np.ascontiguousarray(packed, dtype=np.uint8)
+        d_in = torch.from_numpy(packed).to(dev) if packed.size else torch.zeros(16, dtype=torch.uint8,
+                                                                                device=dev)
+        out_size = np.asarray(out_sizes, dtype=np.uint64)
+        out_off = np.zeros_like(out_size)
+        if out_size.size:
+            out_off[1:] = np.cumsum(out_size)[:-1]
+        total = int(out_size.sum()) if out_size.size else 0
+        d_out = torch.full((max(total, 16),), fill, dtype=torch.uint8, device=dev)
+        return cls(d_in, in_off, in_size, d_out, out_off, out_size)
+
+    @classmethod
+    def from_host(cls, tiles: Sequence, out_sizes, device: int = 0, fill: int = 0) -> "TileBatch":
+        bufs = [np.frombuffer(bytes(t), dtype=np.uint8) if not isinstance(t, np.ndarray)
+                else np.ascontiguousarray(t).view(np.uint8).reshape(-1) for t in tiles]
+        sizes = np.array([b.size for b in bufs], dtype=np.uint64)
+        # 16-byte aligned packing keeps every tile start aligned like a VFS read
+        al = (sizes + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+        offs = np.zeros_like(sizes)
+        if sizes.size:
+            offs[1:] = np.cumsum(al)[:-1]
+        packed = np.zeros(int(al.sum()) if al.size else 0, dtype=np.uint8)
+        for b, o in zip(bufs, offs):
+            packed[int(o):int(o) + b.size] = b
+        return cls.from_packed(packed, offs, sizes, out_sizes, device=device, fill=fill)
+
+    def output(self, i: int) -> np.ndarray:
+        o, n = int(self.out_off[i]), int(self.out_size[i])
+        return self.d_out[o:o + n].cpu().numpy()
+
+    def outputs_host(self) -> np.ndarray:
+        return self.d_out.cpu().numpy()
+
+
+class Context:
+    """tdbg_context: per-device scratch, status arrays, timing."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.tdbg_context_create(device, ctypes.byref(h)), "tdbg_context_create")
+        self.h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            lib.tdbg_context_destroy(h)
+            self.h = None
+
+    @staticmethod
+    def _stream(stream) -> int:
+        if stream is not None:
+            return int(stream)
+        import torch
+        return int(torch.cuda.current_stream().cuda_stream)
+
+    def unfilter(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
+                 stream=None) -> np.ndarray:
+        """Synchronous unfilter; returns the per-tile status array."""
+        st = np.zeros(max(batch.ntiles, 1), dtype=np.int32)
+        pin, psz, pout, posz = batch.ptrs()
+        rc = lib.tdbg_unfilter_tiles_sync(
+            self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
+            TILE_OFFSETS if offsets_tiles else 0,
+            st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self._stream(stream))
+        if rc and not st[: batch.ntiles].any():
+            _check(rc, "tdbg_unfilter_tiles_sync")
+        return st[: batch.ntiles]
+
+    def unfilter_async(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
+                       stream=None) -> None:
+        pin, psz, pout, posz = batch.ptrs()
+        _check(lib.tdbg_unfilter_tiles_async(
+            self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
+            TILE_OFFSETS if offsets_tiles else 0, batch.d_status.data_ptr(),
+            self._stream(stream)), "tdbg_unfilter_tiles_async")
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        _check(lib.tdbg_context_last_kernel_ms(self.h, ctypes.byref(ms)), "last_kernel_ms")
+        return float(ms.value)
+
+    def unfilter_host(self, dp: DevicePipeline, in_ptrs: np.ndarray, in_size: np.ndarray,
+                      out_ptrs: np.ndarray, out_size: np.ndarray, offsets_tiles: bool = False,
+                      batch_bytes: int = 0) -> np.ndarray:
+        """Host-resident end-to-end (pinned H2D, unfilter, D2H)."""
+        n = int(in_size.size)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
+        isz = np.ascontiguousarray(in_size, dtype=np.uint64)
+        op = np.ascontiguousarray(out_ptrs, dtype=np.uint64)
+        osz = np.ascontiguousarray(out_size, dtype=np.uint64)
+        rc = lib.tdbg_unfilter_tiles_host(
+            self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data, osz.ctypes.data,
+            TILE_OFFSETS if offsets_tiles else 0,
+            st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), batch_bytes)
+        if rc and not st[:n].any():
+            _check(rc, "tdbg_unfilter_tiles_host")
+        return st[:n]
+
+
+def unfilter_multi_gpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, devices,
+                       offsets_tiles: bool = False, batch_bytes: int = 0) -> np.ndarray:
+    n = int(np.asarray(in_size).size)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
+    isz = np.ascontiguousarray(in_size, dtype=np.uint64)
+    op = np.ascontiguousarray(out_ptrs, dtype=np.uint64)
+    osz = np.ascontiguousarray(out_size, dtype=np.uint64)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    rc = lib.tdbg_unfilter_tiles_multi_gpu(
+        dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data, osz.ctypes.data,
+        TILE_OFFSETS if offsets_tiles else 0, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+        devs, len(devices), batch_bytes)
+    if rc and not st[:n].any():
+        _check(rc, "tdbg_unfilter_tiles_multi_gpu")
+    return st[:n]
+
+
+def device_count() -> int:
+    n = ctypes.c_int32()
+    _check(lib.tdbg_device_count(ctypes.byref(n)), "tdbg_device_count")
+    return int(n.value)
