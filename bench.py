@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident unfilter of the BASELINE 3-stage pipeline.
+
+Workload (BASELINE.json configs[4]): dense int32 tiles of
+64 KiB (one chunk each), pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)],
+12,500 tiles per GPU (C5's 100k tiles over 8 GPUs; weak scaling).  A step is
+one unfilter pass (one tdbg_unfilter_tiles_async launch) over the rank's
+12,500 resident tiles.  The headline `value` is the "rand" data variant
+(every byte moves; DD falls back to raw); the "ramp" variant is reported
+beside it.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def build_batch(engine, variant: str, ntiles: int, nunique: int, device: int, seed: int):
+    import workloads as W
+    pool, vals = W.c5_pool(variant, nunique, seed=seed)
+    idx = np.arange(ntiles) % nunique
+    sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
+    al = (sizes + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(al)[:-1]
+    packed = np.zeros(int(al.sum()), dtype=np.uint8)
+    pool_np = [np.frombuffer(p, dtype=np.uint8) for p in pool]
+    for k, (i, o) in enumerate(zip(idx, offs)):
+        packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
+    batch = engine.TileBatch.from_packed(packed, offs, sizes, [W.TILE_BYTES] * ntiles,
+                                         device=device)
+    return batch, pool, vals, idx, packed, offs, sizes
+
+
+def verify(batch, vals, idx) -> None:
+    out = batch.d_out[: len(idx) * 65536].view(-1, 65536)
+    first = {}
+    for t, i in enumerate(idx):
+        if i not in first:
+            first[i] = t
+    for i, t in first.items():
+        got = out[t].cpu().numpy()
+        if not np.array_equal(got, vals[i].view(np.uint8)):
+            raise SystemExit(f"bench verification failed: tile {t} differs from its source values")
+
+
+def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: int):
+    import torch
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        ctx.unfilter_async(dp, batch, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    st = batch.d_status[: batch.ntiles].cpu().numpy()
+    if st.any():
+        raise SystemExit(f"device status nonzero: {np.unique(st)}")
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        evs[s][0].record(stream)
+        ctx.unfilter_async(dp, batch, stream=stream.cuda_stream)
+        evs[s][1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, float(np.mean(kern_ms)), kern_ms
+
+
+def cpu_baseline(packed, offs, sizes, ntiles_sample: int, threads: int, min_seconds: float = 1.5):
+    """Oracle (CPU restatement, test infrastructure) on a bounded sample."""
+    from oracle import oracle as O
+    import workloads as W
+    op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+    n = min(ntiles_sample, offs.size)
+    out = np.zeros(n * W.TILE_BYTES, dtype=np.uint8)
+    out_off = np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES)
+    out_size = np.full(n, W.TILE_BYTES, dtype=np.uint64)
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        rc, st = op.unfilter_tiles_mt(packed, offs[:n], sizes[:n], out, out_off, out_size, threads)
+        if rc:
+            raise SystemExit(f"cpu baseline failed: {rc}")
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    gib = reps * n * W.TILE_BYTES / 2**30
+    return gib / el, reps * n, el
+
+
+def load_traffic(variant: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(variant, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tiles-per-gpu", type=int, default=12500)
+    ap.add_argument("--unique", type=int, default=128)
+    ap.add_argument("--variants", default="rand,ramp")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--e2e", action="store_true", help="also time host-resident end-to-end")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+    else:
+        torch.cuda.set_device(0)
+    from tiledb_amd import engine
+    import workloads as W
+
+    dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)  # INT32, cell 4
+    ctx = engine.Context(local)
+    variants = [v for v in args.variants.split(",") if v]
+    res = {}
+    for vi, var in enumerate(variants):
+        batch, pool, vals, idx, packed, offs, sizes = build_batch(
+            engine, var, args.tiles_per_gpu, args.unique, local, seed=5 + 1000 * rank + vi)
+        ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
+        verify(batch, vals, idx)
+        elapsed, kern_ms, _ = time_device(engine, ctx, dp, batch, args.steps, args.warmup, dist,
+                                          world)
+        unf = float(args.tiles_per_gpu) * W.TILE_BYTES
+        b_alg = float(sizes.sum()) + unf
+        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, b_alg=b_alg, unf=unf,
+                        packed=packed, offs=offs, sizes=sizes)
+        if args.e2e:
+            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, args)
+        del batch
+        torch.cuda.empty_cache()
+
+    head = variants[0]
+    r = res[head]
+    ms_per_step = r["elapsed"] / args.steps * 1e3
+    total_unf = r["unf"] * world
+    value = total_unf / (r["elapsed"] / args.steps) / 2**30
+    achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
+    traffic = load_traffic(head)
+    line = {
+        "metric": "GiB/s unfiltered tile bytes (device-resident), 64 KiB chunks, 3-stage pipeline",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": f"synthetic C5 '{head}' tiles ({args.unique} unique, replicated), numpy-encoded",
+        "config": {
+            "workload": "C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
+                        "64 KiB tiles (1 chunk), device-resident",
+            "tiles_per_gpu": args.tiles_per_gpu,
+            "variant": head,
+            "parallelism": f"tile-shard x{world} (no collectives)",
+            "filtered_bytes_per_gpu": int(r["sizes"].sum()),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(r["kern_ms"], 4),
+            "algorithmic_bytes_per_launch": int(r["b_alg"]),
+        },
+    }
+    for var in variants[1:]:
+        rv = res[var]
+        line["config"][f"{var}_GiBps"] = round(
+            rv["unf"] * world / (rv["elapsed"] / args.steps) / 2**30, 2)
+        line["config"][f"{var}_roofline_frac"] = round(
+            rv["b_alg"] / (rv["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if args.e2e:
+        line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        cpu, ntl, el = cpu_baseline(r["packed"], r["offs"], r["sizes"], 2048, threads)
+        line["cpu_baseline"] = {
+            "value": round(cpu, 3),
+            "unit": "GiB/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"{ntl} C5 '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s on "
+                      f"{threads} threads, oracle/ C restatement",
+        }
+    if rank == 0:
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def e2e(engine, ctx, dp, packed, offs, sizes, args):
+    """Host-resident end-to-end: pinned H2D + unfilter + D2H (PCIe-inclusive)."""
+    import torch
+    import workloads as W
+    n = offs.size
+    hin = torch.from_numpy(packed).pin_memory()
+    hout = torch.empty(n * W.TILE_BYTES, dtype=torch.uint8).pin_memory()
+    in_ptrs = offs + np.uint64(hin.data_ptr())
+    out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES) + np.uint64(hout.data_ptr())
+    osz = np.full(n, W.TILE_BYTES, dtype=np.uint64)
+    ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=256 << 20)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=256 << 20)
+    el = time.perf_counter() - t0
+    assert not st.any()
+    return round(reps * n * W.TILE_BYTES / el / 2**30, 2)
+
+
+if __name__ == "__main__":
+    main()

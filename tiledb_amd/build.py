@@ -17,7 +17,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 
 SOURCES = ["tdbg_kernels.hip", "tdbg_fast.hip", "tdbg_host.cpp"]
-HEADERS = ["tdbg_desc.h", "tdbg_device.h"]
+HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h"]
 
 
 def _stale() -> bool:
