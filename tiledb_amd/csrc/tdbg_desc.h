@@ -37,6 +37,8 @@ struct tdbg_plan {
   tdbg_stage s[TDBG_MAX_FILTERS];
 };
 
+#define TDBG_E_FALLBACK 100  // internal: fast path declined the tile
+
 enum tdbg_fast_kind : uint32_t {
   TDBG_FAST_NONE = 0,
 };
@@ -56,6 +58,8 @@ struct KParams {
   uint8_t* scratch;
   uint64_t slot_bytes;
   uint32_t slot_cap, md_cap, tab_cap;
+  uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
+  uint32_t fixup;     // general kernel: only tiles whose status is TDBG_E_FALLBACK
   tdbg_plan plan;
 };
 

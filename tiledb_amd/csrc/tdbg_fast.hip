@@ -20,7 +20,6 @@
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
 #include "tdbg_device.h"
-#include "tdbg_general.h"
 
 #include <type_traits>
 
@@ -49,6 +48,16 @@ struct View {
   uint32_t base, n;  // bytes [base, base+n) of L.X
 };
 
+// Thread index, opaque to the optimizer: the per-thread index math of the
+// unrolled stage loops is tile-invariant, and hoisting it out of the
+// persistent tile loop would pin (and spill) dozens of registers for the
+// whole kernel.  An empty asm on a copy keeps it inside the loop.
+__device__ __forceinline__ uint32_t tid_() {
+  uint32_t t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // ---------------------------------------------------------------------------
 // LDS byte access at arbitrary offsets (aligned dword reads + alignbyte)
 // ---------------------------------------------------------------------------
@@ -72,6 +81,28 @@ __device__ __forceinline__ uint64_t ldsn(const uint8_t* X, uint32_t off, uint32_
   return k == 8 ? v : (v & ((1ull << (8 * k)) - 1));
 }
 
+// explicit global (address space 1) accesses: global_load/store, not flat
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u g_cu4;
+typedef __attribute__((address_space(1))) v4u g_u4;
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+
+__device__ __forceinline__ uint64_t gldn(const uint8_t* p, uint32_t k) {
+  const uintptr_t a = (uintptr_t)p;
+  const g_cu32* q = (const g_cu32*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t nd = (sh + k + 3) >> 2;
+  const uint32_t d0 = q[0];
+  const uint32_t d1 = nd > 1 ? q[1] : 0u;
+  const uint32_t d2 = nd > 2 ? q[2] : 0u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  uint64_t v = ((uint64_t)hi << 32) | lo;
+  if (k < 8) v &= (1ull << (8 * k)) - 1;
+  return v;
+}
+
 __device__ __forceinline__ bool block_any(bool p) { return __syncthreads_or(p ? 1 : 0) != 0; }
 
 // ---------------------------------------------------------------------------
@@ -87,18 +118,21 @@ __device__ __forceinline__ bool load_to_lds(uint8_t* X, uint32_t cap, const uint
   const uint32_t cnt = (uint32_t)((a1 - a0) >> 4);
   *base = (uint32_t)((uintptr_t)g - a0);
   if (cnt * 16 > cap) return false;
-  const uint4* src = (const uint4*)a0;
+  const g_cu4* src = (const g_cu4*)a0;
   constexpr int LU = (XCAP / 16 + FNT - 1) / FNT;
-  uint4 v[LU];
+  // Issue every load first (clamped to a valid unit: no divergent control
+  // flow around the loads, so they stay in registers), then the LDS stores.
+  const uint32_t t = tid_();
+  v4u v[LU];
 #pragma unroll
   for (int k = 0; k < LU; k++) {
-    const uint32_t u = threadIdx.x + k * FNT;
-    if (u < cnt) v[k] = src[u];
+    const uint32_t u = t + k * FNT;
+    v[k] = src[u < cnt ? u : cnt - 1];
   }
 #pragma unroll
   for (int k = 0; k < LU; k++) {
-    const uint32_t u = threadIdx.x + k * FNT;
-    if (u < cnt) *(uint4*)(X + 16 * u) = v[k];
+    const uint32_t u = t + k * FNT;
+    if (u < cnt) *(v4u*)(X + 16 * u) = v[k];
   }
   return true;
 }
@@ -107,7 +141,8 @@ __device__ __forceinline__ bool load_to_lds(uint8_t* X, uint32_t cap, const uint
 // and unaligned chunk destinations.
 __device__ __forceinline__ void store_unit(uint8_t* gout, uint32_t n, uint32_t off, uint4 v) {
   if (off + 16 <= n && (((uintptr_t)(gout + off)) & 15) == 0) {
-    *(uint4*)(gout + off) = v;
+    v4u x = {v.x, v.y, v.z, v.w};
+    *(g_u4*)(gout + off) = x;
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -116,7 +151,7 @@ __device__ __forceinline__ void store_unit(uint8_t* gout, uint32_t n, uint32_t o
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const uint32_t o = off + 4 * d + b;
-      if (o < n) gout[o] = (uint8_t)(w[d] >> (8 * b));
+      if (o < n) ((g_u8*)gout)[o] = (uint8_t)(w[d] >> (8 * b));
     }
 }
 
@@ -130,7 +165,7 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
   constexpr int UD = UB / 4;
   if (final) {
     const uint32_t nu = (n + UB - 1) / UB;
-    for (uint32_t u = threadIdx.x; u < nu; u += FNT) {
+    for (uint32_t u = tid_(); u < nu; u += FNT) {
       uint32_t w[UD];
       fn(u, w);
 #pragma unroll
@@ -139,17 +174,21 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
     }
     return;
   }
-  constexpr int NU = FP / UB;
-  uint32_t r[FPD];
-  const uint32_t s0 = threadIdx.x * FP;
+  // slice = whole units, >= 144 B so FNT slices cover XCAP
+  constexpr int SLB = UB >= 64 ? 192 : (UB == 32 ? 160 : 144);
+  constexpr int NU = SLB / UB;
+  constexpr int RD = SLB / 4;
+  uint32_t r[RD];
+  const uint32_t s0 = tid_() * SLB;
 #pragma unroll
   for (int k = 0; k < NU; k++) {
-    const uint32_t u = threadIdx.x * NU + k;
+    const uint32_t u = tid_() * NU + k;
     if (u * UB < n) fn(u, *(uint32_t(*)[UD])(r + k * UD));
+    __builtin_amdgcn_sched_barrier(0);  // keep each unit's loads local
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < FPD / 4; k++) {
+  for (int k = 0; k < RD / 4; k++) {
     const uint32_t o = s0 + 16 * k;
     if (o < n) *(uint4*)(L.X + o) = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
   }
@@ -158,7 +197,7 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
 
 // Copy a view to the final output (pass-through / raw stages as filter 0).
 __device__ void final_copy(FastLds& L, View v, uint8_t* gout) {
-  for (uint32_t u = threadIdx.x; u * 16 < v.n; u += FNT) {
+  for (uint32_t u = tid_(); u * 16 < v.n; u += FNT) {
     const uint32_t o = v.base + 16 * u;
     uint4 x;
     if ((o & 15) == 0) x = *(const uint4*)(L.X + o);
@@ -189,7 +228,7 @@ __device__ __forceinline__ uint32_t unshuf_byte(const uint8_t* X, uint32_t base,
 }
 
 template <int TS>
-__device__ __attribute__((noinline)) bool f_byteshuffle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                               uint8_t* gout, uint32_t cap) {
   if (mn < 8) return false;
   const uint32_t np = lds32(L.MD, mo), ps = lds32(L.MD, mo + 4);
@@ -281,7 +320,7 @@ __device__ __attribute__((noinline)) bool f_byteshuffle(FastLds& L, View& cur, u
 // bitshuffle^-1 (8192-B blocks; bitshuffle_filter.cc:168-212)
 // ---------------------------------------------------------------------------
 template <int TS>
-__device__ __attribute__((noinline)) bool f_bitshuffle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_bitshuffle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                              uint8_t* gout, uint32_t cap) {
   if (mn < 8) return false;
   const uint32_t np = lds32(L.MD, mo), ps = lds32(L.MD, mo + 4);
@@ -350,9 +389,9 @@ __device__ __forceinline__ uint64_t bwr_elem(const uint8_t* X, uint32_t base, ui
 }
 
 template <int W, bool SGN>
-__device__ __attribute__((noinline)) bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                       uint8_t* gout, uint32_t cap, uint32_t dts) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tid_();
   if (mn < 8) return false;
   const uint32_t orig = lds32(L.MD, mo), nw = lds32(L.MD, mo + 4);
   const uint32_t E = dts + 5;
@@ -453,7 +492,7 @@ __device__ __attribute__((noinline)) bool f_bwr(FastLds& L, View& cur, uint32_t&
 // Double-delta tuple (E, X) exclusive scan; cnt elements per thread.
 __device__ __forceinline__ void block_ddscan_n(uint64_t& E, uint64_t& Xs, uint64_t cnt,
                                                uint64_t* red) {
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
   uint64_t iE = E, iX = Xs;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -480,7 +519,7 @@ __device__ __forceinline__ void block_ddscan_n(uint64_t& E, uint64_t& Xs, uint64
 // Segmented sum (positive delta windows): aggregate (has_head, sum after the
 // last head).  Exclusive scan; returns the carry into this thread's slice.
 __device__ __forceinline__ uint64_t block_segscan(bool has, uint64_t sum, uint64_t* red) {
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
   uint32_t ih = has;
   uint64_t is = sum;
 #pragma unroll
@@ -527,7 +566,7 @@ __device__ __forceinline__ void rset(uint32_t (&r)[N], int k, uint64_t v) {
 // write a slice register file to X[0, n) (after the barrier the caller issues)
 template <int N>
 __device__ __forceinline__ void slice_store(FastLds& L, const uint32_t (&r)[N], uint32_t n) {
-  const uint32_t s0 = threadIdx.x * (4 * N);
+  const uint32_t s0 = tid_() * (4 * N);
 #pragma unroll
   for (int k = 0; k < N / 4; k++) {
     const uint32_t o = s0 + 16 * k;
@@ -540,9 +579,9 @@ __device__ __forceinline__ void slice_store(FastLds& L, const uint32_t (&r)[N], 
 // TAB[w] = {first lo, first hi, nb, raw}
 // ---------------------------------------------------------------------------
 template <int W>
-__device__ __attribute__((noinline)) bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap, uint32_t dts) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tid_();
   if (mn < 4) return false;
   const uint32_t nw = lds32(L.MD, mo);
   const uint32_t E = dts + 4;
@@ -608,6 +647,7 @@ __device__ __attribute__((noinline)) bool f_pd(FastLds& L, View& cur, uint32_t& 
         run += rget<W>(r, k);
         rset<W>(r, k, run);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   __syncthreads();
@@ -735,7 +775,7 @@ struct DDReader {
 // the codes.  Arithmetic is modulo 2^(8W) (32-bit lanes for W <= 4), which is
 // exactly the reference's (T)(dd + 2*x[i-1] - x[i-2]) (dd_compressor.cc:355).
 template <int W>
-__device__ __attribute__((noinline)) void dd_decode_part(FastLds& L, uint32_t src, uint32_t b,
+__device__ __forceinline__ void dd_decode_part(FastLds& L, uint32_t src, uint32_t b,
                                                           uint64_t num) {
   typedef typename std::conditional<(W == 8), uint64_t, uint32_t>::type U;
   constexpr int EP = SP / W;
@@ -743,7 +783,7 @@ __device__ __attribute__((noinline)) void dd_decode_part(FastLds& L, uint32_t sr
   const U x0 = (U)ldsn(X, src + 9, W), x1 = (U)ldsn(X, src + 9 + W, W);
   const uint32_t bs = src + 9 + 2 * W;
   const U dinit = x1 - x0, xinit = x0 - dinit;
-  const uint32_t i0 = threadIdx.x * EP;
+  const uint32_t i0 = tid_() * EP;
   const uint32_t first = i0 < 2 ? 2 : i0;
   const uint64_t s0 = (uint64_t)(first - 2) * (b + 1);
   // pass 1: aggregates only
@@ -758,6 +798,7 @@ __device__ __attribute__((noinline)) void dd_decode_part(FastLds& L, uint32_t sr
       if (i >= 2 && i < num) e = (U)rd.template next<(W <= 4)>(b);
       E += e;
       Xs += E;
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   uint64_t E64 = E, X64 = Xs;
@@ -779,6 +820,7 @@ __device__ __attribute__((noinline)) void dd_decode_part(FastLds& L, uint32_t sr
       d += e;
       x += d;
       rset<W>(r, k, (uint64_t)x);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   __syncthreads();
@@ -790,7 +832,7 @@ __device__ __attribute__((noinline)) void dd_decode_part(FastLds& L, uint32_t sr
 // compression filter (DD / RLE) -- compression_filter.cc:303-347,413-486
 // ---------------------------------------------------------------------------
 template <int W>
-__device__ __attribute__((noinline)) bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap);
 
 // Reads the compression md header (compression_filter.cc:323-347) into
@@ -806,7 +848,7 @@ __device__ bool comp_header(FastLds& L, View cur, uint32_t mo, uint32_t mn, uint
   md_total = 0;
   for (uint32_t i = 0; i <= nmd; i++) {
     const uint32_t un = lds32(L.MD, mo + 8 + 8 * i), cn = lds32(L.MD, mo + 12 + 8 * i);
-    if (threadIdx.x == 0) {
+    if (tid_() == 0) {
       L.pairs[3 * i] = un;
       L.pairs[3 * i + 1] = cn;
       L.pairs[3 * i + 2] = p;
@@ -821,7 +863,7 @@ __device__ bool comp_header(FastLds& L, View cur, uint32_t mo, uint32_t mn, uint
 }
 
 template <int W>
-__device__ __attribute__((noinline)) bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap) {
   uint32_t nmd, src, c, u, mdt;
   if (!comp_header(L, cur, mo, mn, nmd, src, c, u, mdt)) return false;
@@ -839,7 +881,7 @@ __device__ __attribute__((noinline)) bool f_dd(FastLds& L, View& cur, uint32_t& 
   if (bad) return false;
   // metadata parts: thread 0, serially, into MD[0, mdt)
   __syncthreads();  // every thread has read the header
-  if (threadIdx.x == 0) {
+  if (tid_() == 0) {
     bool ok = true;
     uint32_t o = 0;
     for (uint32_t i = 0; i < nmd; i++) {
@@ -866,7 +908,7 @@ __device__ __attribute__((noinline)) bool f_dd(FastLds& L, View& cur, uint32_t& 
   return true;
 }
 
-__device__ __attribute__((noinline)) bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+__device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                       uint8_t* gout, uint32_t cap, uint32_t cs) {
   uint32_t nmd, src, c, u, mdt;
   if (cs != 1 && cs != 2 && cs != 4 && cs != 8) return false;
@@ -877,7 +919,7 @@ __device__ __attribute__((noinline)) bool f_rle(FastLds& L, View& cur, uint32_t&
   // run starts (cells)
   uint64_t acc = 0;
   for (uint32_t r0 = 0; r0 < nr; r0 += FNT) {
-    const uint32_t r = r0 + threadIdx.x;
+    const uint32_t r = r0 + tid_();
     uint32_t len = 0;
     if (r < nr) len = ((uint32_t)L.X[src + r * rs + cs] << 8) | L.X[src + r * rs + cs + 1];
     uint64_t t;
@@ -885,10 +927,10 @@ __device__ __attribute__((noinline)) bool f_rle(FastLds& L, View& cur, uint32_t&
     if (r < nr) start[r] = (uint32_t)ex;
     acc += t;
   }
-  if (threadIdx.x == 0) start[nr] = (uint32_t)acc;
+  if (tid_() == 0) start[nr] = (uint32_t)acc;
   if (block_any(acc * cs != u)) return false;
   // metadata parts (thread 0)
-  if (threadIdx.x == 0) {
+  if (tid_() == 0) {
     bool ok = true;
     uint32_t o = 0;
     for (uint32_t i = 0; i < nmd; i++) {
@@ -931,13 +973,49 @@ __device__ __attribute__((noinline)) bool f_rle(FastLds& L, View& cur, uint32_t&
 }
 
 // ---------------------------------------------------------------------------
-// chunk driver
+// compile-time pipeline specs
 // ---------------------------------------------------------------------------
-// Returns true when the chunk was fully unfiltered into gout; false = fall
-// back to the general interpreter (nothing was written to gout).
-__device__ __attribute__((noinline)) bool f_chunk(const tdbg_plan& P, const uint8_t* gmd, uint32_t ml,
-                        const uint8_t* gdata, uint32_t fl, uint8_t* gout, uint32_t orig,
-                        FastLds& L) {
+// Stage code: kind | W << 4 | signed << 8 (0 = no stage).  A spec lists the
+// stages in pipeline order (filter 0 first); the fused kernel for a spec
+// inlines exactly those stages, so register allocation and LDS address-space
+// inference see one small straight-line program.
+#define SC(kind, w, sg) ((kind) | ((w) << 4) | ((sg) << 8))
+
+template <int CODE>
+__device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn,
+                                          bool final, uint8_t* gout, uint32_t cap,
+                                          const tdbg_stage& s) {
+  constexpr int K = CODE & 15, W = (CODE >> 4) & 15, SG = (CODE >> 8) & 1;
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (K == TDBG_K_PASS) {
+    if (final) {
+      if (cur.n > cap) return false;
+      final_copy(L, cur, gout);
+    }
+    return true;
+  } else if constexpr (K == TDBG_K_BYTESHUFFLE) {
+    return f_byteshuffle<W>(L, cur, mo, mn, final, gout, cap);
+  } else if constexpr (K == TDBG_K_BITSHUFFLE) {
+    return f_bitshuffle<W>(L, cur, mo, mn, final, gout, cap);
+  } else if constexpr (K == TDBG_K_BWR) {
+    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts);
+  } else if constexpr (K == TDBG_K_PD) {
+    return f_pd<W>(L, cur, mo, mn, final, gout, cap, s.dts);
+  } else if constexpr (K == TDBG_K_DD) {
+    return f_dd<W>(L, cur, mo, mn, final, gout, cap);
+  } else if constexpr (K == TDBG_K_RLE) {
+    return f_rle(L, cur, mo, mn, final, gout, cap, (uint32_t)s.cs);
+  } else {
+    return false;
+  }
+}
+
+// Returns true when the chunk was fully unfiltered into gout; false = the
+// general interpreter must redo the tile (nothing was written to gout).
+template <int S0, int S1, int S2, int S3>
+__device__ __forceinline__ bool f_chunk(const tdbg_plan& P, const uint8_t* gmd, uint32_t ml,
+                                        const uint8_t* gdata, uint32_t fl, uint8_t* gout,
+                                        uint32_t orig, FastLds& L, uint32_t dbg_stop) {
   if (ml > MDCAP - 16) return false;
   uint32_t dbase, mbase;
   const bool ok_d = load_to_lds(L.X, XCAP, gdata, fl, &dbase);
@@ -946,88 +1024,37 @@ __device__ __attribute__((noinline)) bool f_chunk(const tdbg_plan& P, const uint
   __syncthreads();
   View cur = {dbase, fl};
   uint32_t mo = mbase, mn = ml;
-  if (P.nstages == 0) {
-    if (fl > orig) return false;
-    final_copy(L, cur, gout);
-    return true;
+  if (dbg_stop == 1) return true;  // timing ablation: load only
+  // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
+  if constexpr (S3 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
+    if (!run_stage<S3>(L, cur, mo, mn, false, gout, orig, P.s[3])) return false;
+    if (cur.n > XCAP) return false;
   }
-  for (int k = (int)P.nstages - 1; k >= 0; k--) {
-    const tdbg_stage& s = P.s[k];
-    const bool final = k == 0;
-    bool ok = false;
-    switch (s.kind) {
-      case TDBG_K_PASS:
-        if (final) {
-          if (cur.n > orig) return false;
-          final_copy(L, cur, gout);
-        }
-        ok = true;
-        break;
-      case TDBG_K_BYTESHUFFLE:
-        if (s.w == 4) ok = f_byteshuffle<4>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 8) ok = f_byteshuffle<8>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 2) ok = f_byteshuffle<2>(L, cur, mo, mn, final, gout, orig);
-        else ok = f_byteshuffle<1>(L, cur, mo, mn, final, gout, orig);
-        break;
-      case TDBG_K_BITSHUFFLE:
-        if (s.w == 4) ok = f_bitshuffle<4>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 8) ok = f_bitshuffle<8>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 2) ok = f_bitshuffle<2>(L, cur, mo, mn, final, gout, orig);
-        else ok = f_bitshuffle<1>(L, cur, mo, mn, final, gout, orig);
-        break;
-      case TDBG_K_BWR:
-        if (s.w == 4) ok = s.sgn ? f_bwr<4, true>(L, cur, mo, mn, final, gout, orig, s.dts)
-                                 : f_bwr<4, false>(L, cur, mo, mn, final, gout, orig, s.dts);
-        else if (s.w == 8) ok = s.sgn ? f_bwr<8, true>(L, cur, mo, mn, final, gout, orig, s.dts)
-                                      : f_bwr<8, false>(L, cur, mo, mn, final, gout, orig, s.dts);
-        else ok = s.sgn ? f_bwr<2, true>(L, cur, mo, mn, final, gout, orig, s.dts)
-                        : f_bwr<2, false>(L, cur, mo, mn, final, gout, orig, s.dts);
-        break;
-      case TDBG_K_PD:
-        if (s.w == 8) ok = f_pd<8>(L, cur, mo, mn, final, gout, orig, s.dts);
-        else if (s.w == 4) ok = f_pd<4>(L, cur, mo, mn, final, gout, orig, s.dts);
-        else if (s.w == 2) ok = f_pd<2>(L, cur, mo, mn, final, gout, orig, s.dts);
-        else ok = f_pd<1>(L, cur, mo, mn, final, gout, orig, s.dts);
-        break;
-      case TDBG_K_DD:
-        if (s.w == 4) ok = f_dd<4>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 8) ok = f_dd<8>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 2) ok = f_dd<2>(L, cur, mo, mn, final, gout, orig);
-        else if (s.w == 1) ok = f_dd<1>(L, cur, mo, mn, final, gout, orig);
-        break;
-      case TDBG_K_RLE:
-        ok = f_rle(L, cur, mo, mn, final, gout, orig, (uint32_t)s.cs);
-        break;
-      default:
-        ok = false;
-    }
-    if (!ok) return false;
-    if (!final && cur.n > XCAP) return false;
+  if constexpr (S2 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
+    if (!run_stage<S2>(L, cur, mo, mn, false, gout, orig, P.s[2])) return false;
+    if (cur.n > XCAP) return false;
   }
-  return true;
+  if constexpr (S1 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
+    if (!run_stage<S1>(L, cur, mo, mn, false, gout, orig, P.s[1])) return false;
+    if (cur.n > XCAP) return false;
+  }
+  if (dbg_stop > 1) return true;
+  return run_stage<S0>(L, cur, mo, mn, true, gout, orig, P.s[0]);
 }
 
+template <int S0, int S1, int S2, int S3>
 __global__ void __launch_bounds__(FNT, 4)
-unfilter_fast_kernel(const KParams kp) {
+unfilter_fused_kernel(const KParams kp) {
   __shared__ FastLds L;
-  __shared__ Shared<FNT> gsh;
-  Slot sl;
-  uint8_t* sbase = kp.scratch + (uint64_t)blockIdx.x * kp.slot_bytes;
-  sl.slot_cap = kp.slot_cap;
-  sl.md_cap = kp.md_cap;
-  sl.tab_cap = kp.tab_cap;
-  sl.buf[0] = sbase;
-  sl.buf[1] = sbase + kp.slot_cap;
-  sl.md[0] = sbase + 2ull * kp.slot_cap;
-  sl.md[1] = sl.md[0] + kp.md_cap;
-  sl.tab = sl.md[1] + kp.md_cap;
   for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
     const uint64_t t = kp.tile_list ? kp.tile_list[j] : j;
     const uint8_t* in = kp.in[t];
     const uint64_t fs = kp.in_size[t];
     uint8_t* out = kp.out[t];
     const uint64_t os = kp.out_size[t];
-    uint64_t need = 0;
     int rc = TDBG_OK;
     // Tile::load_chunk_data (tile.cc:280-313)
     uint64_t expected = os;
@@ -1039,11 +1066,11 @@ unfilter_fast_kernel(const KParams kp) {
     if (rc == TDBG_OK) {
       if (fs < 8) rc = TDBG_E_TILE_FORMAT;
       else {
-        nch = ldn(in, 8);
+        nch = gldn(in, 8);
         uint64_t o = 8, total = 0;
         for (uint64_t i = 0; i < nch; i++) {
           if (o + 12 > fs) { rc = TDBG_E_TILE_FORMAT; break; }
-          const uint64_t orig = ldn(in + o, 4), fl = ldn(in + o + 4, 4), ml = ldn(in + o + 8, 4);
+          const uint64_t orig = gldn(in + o, 4), fl = gldn(in + o + 4, 4), ml = gldn(in + o + 8, 4);
           o += 12;
           if (ml > fs - o) { rc = TDBG_E_TILE_FORMAT; break; }
           o += ml;
@@ -1057,44 +1084,111 @@ unfilter_fast_kernel(const KParams kp) {
     if (rc == TDBG_OK) {
       uint64_t o = 8, coff = 0;
       for (uint64_t i = 0; i < nch; i++) {
-        const uint32_t orig = (uint32_t)ldn(in + o, 4), fl = (uint32_t)ldn(in + o + 4, 4),
-                       ml = (uint32_t)ldn(in + o + 8, 4);
+        const uint32_t orig = (uint32_t)gldn(in + o, 4), fl = (uint32_t)gldn(in + o + 4, 4),
+                       ml = (uint32_t)gldn(in + o + 8, 4);
         o += 12;
-        const bool done = f_chunk(kp.plan, in + o, ml, in + o + ml, fl, out + coff, orig, L);
+        const bool done = f_chunk<S0, S1, S2, S3>(kp.plan, in + o, ml, in + o + ml, fl, out + coff,
+                                                  orig, L, kp.dbg_stop);
         __syncthreads();
-        if (!done) {
-          rc = g_chunk<FNT>(kp.plan, in + o, ml, in + o + ml, fl, out + coff, orig, sl, gsh, &need);
-          __syncthreads();
-          if (rc) break;
+        if (!done) {  // the general fixup launch redoes the whole tile
+          rc = TDBG_E_FALLBACK;
+          break;
         }
         o += ml + fl;
         coff += orig;
       }
     }
-    if (threadIdx.x == 0) {
-      if (kp.status) kp.status[t] = rc;
-      if (kp.need) kp.need[t] = need;
-    }
+    if (tid_() == 0 && kp.status) kp.status[t] = rc;
   }
 }
 
 }  // namespace tdbg
 
+// ---------------------------------------------------------------------------
+// spec table: the instantiated fused kernels
+// ---------------------------------------------------------------------------
+#define K_PASS TDBG_K_PASS
+#define K_BYTE TDBG_K_BYTESHUFFLE
+#define K_BIT TDBG_K_BITSHUFFLE
+#define K_BWR TDBG_K_BWR
+#define K_PD TDBG_K_PD
+#define K_DD TDBG_K_DD
+#define K_RLE TDBG_K_RLE
+#define SPECS(X)                                                        \
+  /* C1: [BYTESHUFFLE] int32 / int64 / int16 */                          \
+  X(1, SC(K_BYTE, 4, 0), 0, 0, 0)                                        \
+  X(2, SC(K_BYTE, 8, 0), 0, 0, 0)                                        \
+  X(3, SC(K_BYTE, 2, 0), 0, 0, 0)                                        \
+  /* C2: [BITSHUFFLE, BWR (pass-through on float)] */                    \
+  X(4, SC(K_BIT, 4, 0), SC(K_PASS, 0, 0), 0, 0)                          \
+  X(5, SC(K_BIT, 8, 0), SC(K_PASS, 0, 0), 0, 0)                          \
+  X(6, SC(K_BIT, 4, 0), 0, 0, 0)                                         \
+  X(7, SC(K_BIT, 8, 0), 0, 0, 0)                                         \
+  /* C2i: [BITSHUFFLE, BWR] int32 / int64 */                             \
+  X(8, SC(K_BIT, 4, 0), SC(K_BWR, 4, 1), 0, 0)                           \
+  X(9, SC(K_BIT, 4, 0), SC(K_BWR, 4, 0), 0, 0)                           \
+  X(10, SC(K_BIT, 8, 0), SC(K_BWR, 8, 1), 0, 0)                          \
+  X(11, SC(K_BIT, 8, 0), SC(K_BWR, 8, 0), 0, 0)                          \
+  /* C3a / C3b: [DOUBLE_DELTA] / [RLE] on 64-bit coords */              \
+  X(12, SC(K_DD, 8, 0), 0, 0, 0)                                         \
+  X(13, SC(K_DD, 4, 0), 0, 0, 0)                                         \
+  X(14, SC(K_RLE, 0, 0), 0, 0, 0)                                        \
+  /* C4: [POSITIVE_DELTA, BWR] offsets */                                \
+  X(15, SC(K_PD, 8, 0), SC(K_BWR, 8, 0), 0, 0)                           \
+  X(16, SC(K_PD, 8, 0), SC(K_BWR, 8, 1), 0, 0)                           \
+  X(17, SC(K_PD, 4, 0), SC(K_BWR, 4, 0), 0, 0)                           \
+  X(18, SC(K_PD, 4, 0), SC(K_BWR, 4, 1), 0, 0)                           \
+  /* C5: [BYTESHUFFLE, DOUBLE_DELTA, BWR] */                             \
+  X(19, SC(K_BYTE, 4, 0), SC(K_DD, 4, 0), SC(K_BWR, 4, 1), 0)            \
+  X(20, SC(K_BYTE, 4, 0), SC(K_DD, 4, 0), SC(K_BWR, 4, 0), 0)            \
+  X(21, SC(K_BYTE, 8, 0), SC(K_DD, 8, 0), SC(K_BWR, 8, 1), 0)            \
+  X(22, SC(K_BYTE, 8, 0), SC(K_DD, 8, 0), SC(K_BWR, 8, 0), 0)            \
+  /* DD / RLE followed by BWR, BWR alone */                              \
+  X(23, SC(K_DD, 8, 0), SC(K_BWR, 8, 1), 0, 0)                           \
+  X(24, SC(K_DD, 8, 0), SC(K_BWR, 8, 0), 0, 0)                           \
+  X(25, SC(K_BWR, 4, 1), 0, 0, 0)                                        \
+  X(26, SC(K_BWR, 8, 0), 0, 0, 0)                                        \
+  X(27, SC(K_BWR, 8, 1), 0, 0, 0)
+
+static uint32_t stage_code(const tdbg_stage& s) {
+  switch (s.kind) {
+    case TDBG_K_PASS: return SC(TDBG_K_PASS, 0, 0);
+    case TDBG_K_RLE: return SC(TDBG_K_RLE, 0, 0);
+    case TDBG_K_BWR: return SC(TDBG_K_BWR, s.w, s.sgn ? 1 : 0);
+    case TDBG_K_PD: case TDBG_K_DD: case TDBG_K_BYTESHUFFLE: case TDBG_K_BITSHUFFLE:
+      return SC(s.kind, s.w, 0);
+    default: return 0xffffffffu;
+  }
+}
+
 extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan) {
-  // The fused LDS kernel handles every supported plan (chunks that do not fit
-  // fall back in-kernel); kept as a selector for future specialized kernels.
-  for (uint32_t i = 0; i < plan->nstages; i++)
-    if (plan->s[i].kind == TDBG_K_UNSUPPORTED) return TDBG_FAST_NONE;
-  return 1;
+  if (plan->nstages == 0 || plan->nstages > 4) return TDBG_FAST_NONE;
+  uint32_t c[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < plan->nstages; i++) c[i] = stage_code(plan->s[i]);
+#define MATCH(id, a, b, cc, d) \
+  if (c[0] == (uint32_t)(a) && c[1] == (uint32_t)(b) && c[2] == (uint32_t)(cc) && c[3] == (uint32_t)(d)) return id;
+  SPECS(MATCH)
+#undef MATCH
+  return TDBG_FAST_NONE;
 }
 
 extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus) {
   (void)fast;
-  return (uint32_t)cus * 2;  // two 79 KB workgroups per CU
+  return (uint32_t)cus * 2;  // two ~80 KB workgroups per CU
 }
 
 extern "C" hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid,
                                        hipStream_t stream) {
-  hipLaunchKernelGGL(tdbg::unfilter_fast_kernel, dim3(grid), dim3(tdbg::FNT), 0, stream, *kp);
+  switch (kp->plan.fast) {
+#define LAUNCH(id, a, b, cc, d)                                                              \
+    case id:                                                                               \
+      hipLaunchKernelGGL((tdbg::unfilter_fused_kernel<a, b, cc, d>), dim3(grid), dim3(tdbg::FNT), \
+                         0, stream, *kp);                                                   \
+      break;
+    SPECS(LAUNCH)
+#undef LAUNCH
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

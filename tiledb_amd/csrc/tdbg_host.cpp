@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -417,6 +418,10 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   kp.ntiles = ntiles;
   kp.flags = flags;
   kp.plan = p->plan;
+  {
+    static const char* dbg = getenv("TDBG_DEBUG_STOP");  // timing-only ablation
+    kp.dbg_stop = dbg ? (uint32_t)atoi(dbg) : 0;
+  }
   const bool fast = !force_general && p->plan.fast != 0;
   uint32_t grid;
   if (fast) {
@@ -424,9 +429,10 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   } else {
     grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
   }
-  // The fast kernels fall back to the general interpreter per chunk, so both
-  // need the scratch slots.
-  int rc = ensure_scratch(c, grid);
+  // Scratch slots serve the general interpreter (the general kernel, or the
+  // fixup launch after the fused kernel); size them once, before enqueueing.
+  const uint32_t ggrid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
+  int rc = ensure_scratch(c, fast ? ggrid : grid);
   if (rc) return rc;
   kp.scratch = c->scratch;
   kp.slot_bytes = slot_bytes(c);
@@ -436,6 +442,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   HIP_OK(hipEventRecord(c->ev0, stream));
   hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  if (fast && d_status && !kp.dbg_stop) {
+    // tiles the fused kernel declined (status TDBG_E_FALLBACK) are redone by
+    // the general interpreter, same stream, no host round trip
+    tdbg::KParams g = kp;
+    g.fixup = 1;
+    e = tdbg_launch_general(&g, ggrid, stream);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
+  }
   HIP_OK(hipEventRecord(c->ev1, stream));
   c->timed = true;
   return TDBG_OK;

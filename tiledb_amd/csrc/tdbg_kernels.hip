@@ -38,6 +38,7 @@ unfilter_general_kernel(const KParams kp) {
   sl.tab = sl.md[1] + kp.md_cap;
   for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
     const uint64_t t = kp.tile_list ? kp.tile_list[j] : j;
+    if (kp.fixup && kp.status[t] != TDBG_E_FALLBACK) continue;  // uniform per workgroup
     uint64_t need = 0;
     const int rc = g_tile<GEN_NT>(kp, kp.in[t], kp.in_size[t], kp.out[t], kp.out_size[t], sl, sh, &need);
     __syncthreads();
