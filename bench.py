@@ -82,10 +82,16 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(dist, elapsed, "cuda")
     return elapsed, float(np.mean(kern_ms)), kern_ms
+
+
+def max_over_ranks(dist, x: float, device: str) -> float:
+    """The job's time is its slowest rank's (all_reduce MAX; tests run it on gloo)."""
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def cpu_baseline(packed, offs, sizes, ntiles_sample: int, threads: int, min_seconds: float = 1.5):

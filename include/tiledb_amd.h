@@ -182,6 +182,13 @@ int tdbg_unfilter_tiles_host(tdbg_context* ctx, const tdbg_pipeline* p,
                              const uint64_t* out_size, uint32_t flags,
                              int32_t* host_status, uint64_t batch_bytes);
 
+/* Contiguous tile shards balanced by filtered + unfiltered bytes: shard k is
+ * tiles [cuts[k], cuts[k+1]), cuts has nshards + 1 entries.  Host-only; the
+ * multi-GPU entry point and one-process-per-GPU callers (each rank takes its
+ * shard, no collective on the data path) use the same cut. */
+int tdbg_shard_tiles(uint64_t ntiles, const uint64_t* in_size, const uint64_t* out_size,
+                     uint32_t nshards, uint64_t* cuts);
+
 /* Multi-GPU host-resident end-to-end: tiles are sharded over devices by
  * contiguous ranges balanced by bytes, one host thread + context per device,
  * no inter-GPU communication. */
@@ -201,6 +208,12 @@ int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
 /* Device-side timing of the last tdbg_unfilter_tiles_* launch on ctx, via
  * hipEvents recorded around the kernel on its stream (ms). */
 int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
+
+/* Diagnostics (no reference counterpart): with TDBG_PROF=1 in the
+ * environment, the fused kernel accumulates shader-clock cycles per phase
+ * (0 tile wait, 1 headers, 2-4 intermediate stages, 5 final stage, 6 loop
+ * tail); this sums them over the workgroups of the last launch. */
+int tdbg_debug_phase_clocks(tdbg_context* ctx, uint64_t* out, uint32_t nphases);
 
 /* Device memory helpers for FFI callers without their own allocator. */
 int tdbg_device_alloc(int device, uint64_t bytes, void** out);

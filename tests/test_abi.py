@@ -1,0 +1,131 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what
+include/tiledb_amd.h declares, parses pipeline descriptors like the Python
+mirror of FilterPipeline::deserialize (filter_pipeline.cc:371-409), and
+shards tiles by bytes.  No compute call is made here."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+from tiledb_amd.filter_pipeline import (BitshuffleFilter, BitWidthReductionFilter,
+                                        ByteshuffleFilter, CompressionFilter, Compressor,
+                                        Datatype, FilterPipeline, FilterType,
+                                        PositiveDeltaFilter)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tiledb_amd.h")
+
+
+@pytest.fixture(scope="module")
+def native():
+    so = os.path.join(ROOT, "tiledb_amd", "libtiledb_amd.so")
+    if not os.path.exists(so):
+        from tiledb_amd.build import build
+        build()
+    from tiledb_amd import _native
+    return _native
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tdbg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("tdbg_pipeline_create", "tdbg_unfilter_tiles_async", "tdbg_unfilter_tiles_sync",
+                 "tdbg_unfilter_tiles_host", "tdbg_unfilter_tiles_multi_gpu", "tdbg_shard_tiles"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(native):
+    lib = native.lib
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared but not exported: {missing}"
+
+
+def test_python_signatures_cover_header(native):
+    assert set(declared_functions()) == set(native.SIGNATURES), (
+        set(declared_functions()) ^ set(native.SIGNATURES))
+
+
+def test_status_strings(native):
+    lib = native.lib
+    for code in range(0, 16):
+        s = lib.tdbg_status_str(code)
+        assert s and len(s) >= 2
+    assert lib.tdbg_status_str(0) == b"ok"
+
+
+PIPES = [
+    ("c5", FilterPipeline(65536, [ByteshuffleFilter(), CompressionFilter(Compressor.DOUBLE_DELTA, -1),
+                                  BitWidthReductionFilter(256)]), Datatype.INT32, 4, True),
+    ("bit+bwr", FilterPipeline(65536, [BitshuffleFilter(), BitWidthReductionFilter(128)]),
+     Datatype.UINT64, 8, True),
+    ("pd+bwr", FilterPipeline(65536, [PositiveDeltaFilter(256), BitWidthReductionFilter(256)]),
+     Datatype.UINT32, 4, True),
+    ("rle", FilterPipeline(65536, [CompressionFilter(Compressor.RLE, -1)]), Datatype.INT16, 2, True),
+    ("gzip", FilterPipeline(65536, [CompressionFilter(Compressor.GZIP, 6)]), Datatype.INT32, 4, False),
+    ("zstd+shuffle", FilterPipeline(65536, [ByteshuffleFilter(), CompressionFilter(Compressor.ZSTD, 3)]),
+     Datatype.FLOAT64, 8, False),
+]
+
+
+@pytest.mark.parametrize("name,fp,dt,cs,supported", PIPES, ids=[p[0] for p in PIPES])
+def test_pipeline_create_parses_like_deserialize(native, name, fp, dt, cs, supported):
+    from tiledb_amd.engine import DevicePipeline
+    ser = fp.serialize()
+    dp = DevicePipeline(ser, 23, int(dt), cs)
+    py = FilterPipeline.deserialize(ser, 23, int(dt))
+    assert dp.num_filters == py.size()
+    assert dp.supported == supported
+    cur = Datatype(dt)
+    for i, f in enumerate(py.filters):
+        t, odt = dp.filter_info(i)
+        assert t == int(f.type)
+        cur = f.output_datatype(cur)
+        assert odt == int(cur), (i, odt, cur)
+
+
+def test_pipeline_create_rejects_truncated_descriptor(native):
+    from tiledb_amd.engine import DevicePipeline, EngineError
+    ser = PIPES[0][1].serialize()
+    for cut in (3, 8 + 2, len(ser) - 1):
+        with pytest.raises(EngineError):
+            DevicePipeline(ser[:cut], 23, int(Datatype.INT32), 4)
+
+
+def test_double_delta_reinterpret_byte_by_version(native):
+    """DD carries a reinterpret-datatype byte from format version 20 on."""
+    from tiledb_amd.engine import DevicePipeline
+    v20 = struct.pack("<II", 65536, 1) + struct.pack("<BIBiB", int(FilterType.FILTER_DOUBLE_DELTA),
+                                                     6, int(Compressor.DOUBLE_DELTA), -1,
+                                                     int(Datatype.INT32))
+    dp = DevicePipeline(v20, 20, int(Datatype.UINT8), 1)
+    assert dp.num_filters == 1 and dp.supported
+    v19 = v20[:-1]
+    v19 = v19[:8] + struct.pack("<BI", int(FilterType.FILTER_DOUBLE_DELTA), 5) + v19[13:]
+    dp = DevicePipeline(v19, 19, int(Datatype.INT32), 4)
+    assert dp.num_filters == 1 and dp.supported
+
+
+def test_shard_tiles_balanced_and_covering(native):
+    from tiledb_amd.engine import shard_tiles
+    rng = np.random.default_rng(1)
+    isz = rng.integers(100, 70000, 1000).astype(np.uint64)
+    osz = np.full(1000, 65536, dtype=np.uint64)
+    for n in (1, 2, 3, 8, 1000, 1500):
+        cuts = shard_tiles(isz, osz, n)
+        assert cuts[0] == 0 and cuts[-1] == 1000
+        assert np.all(np.diff(cuts.astype(np.int64)) >= 0)
+        if n <= 8:
+            w = isz + osz
+            per = [int(w[int(a):int(b)].sum()) for a, b in zip(cuts[:-1], cuts[1:])]
+            assert max(per) - min(per) <= 2 * int(w.max())
+    assert list(shard_tiles(np.zeros(0, np.uint64), np.zeros(0, np.uint64), 4)) == [0] * 5

@@ -1,0 +1,97 @@
+"""World-size-2 CPU (gloo) rehearsal of the multi-GPU path.
+
+The path shards: each rank unfilters a contiguous,
+byte-balanced range of tiles (tdbg_shard_tiles) with no collective on the
+data path; the only collectives are the bench's barrier and max-over-ranks
+timing.  Here each rank checks its shard with the CPU oracle (test
+infrastructure), and rank 0 verifies that the gathered shards reproduce the
+single-process result tile for tile.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _tiles():
+    import workloads as W
+    pool_r, vals_r = W.c5_pool("rand", 5, seed=11)
+    pool_m, vals_m = W.c5_pool("ramp", 6, seed=12)
+    tiles = pool_r + pool_m
+    vals = vals_r + vals_m
+    return tiles, vals
+
+
+def _worker(rank: int, world: int, port: int, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        import workloads as W
+        from oracle import oracle as O
+        from tiledb_amd.engine import shard_tiles
+        tiles, vals = _tiles()
+        isz = np.array([len(t) for t in tiles], dtype=np.uint64)
+        osz = np.full(len(tiles), W.TILE_BYTES, dtype=np.uint64)
+        cuts = shard_tiles(isz, osz, world)
+        lo, hi = int(cuts[rank]), int(cuts[rank + 1])
+        op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+        digests = np.zeros(len(tiles), dtype=np.int64)
+        for i in range(lo, hi):
+            rc, out = op.unfilter_tile(tiles[i], W.TILE_BYTES)
+            assert rc == 0
+            assert np.array_equal(out, vals[i].view(np.uint8))
+            digests[i] = int(np.frombuffer(out, dtype=np.uint32).astype(np.uint64).sum()) + 1
+        t = torch.from_numpy(digests)
+        dist.all_reduce(t)  # disjoint shards: the sum is a gather
+        slow = bench.max_over_ranks(dist, float(rank + 1), "cpu")
+        if rank == 0:
+            q.put((t.numpy().tolist(), cuts.tolist(), slow))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_cover_every_tile_once():
+    import sys
+    sys.path.insert(0, ROOT)
+    import workloads as W
+    from oracle import oracle as O
+    O.build()
+    from tiledb_amd import _native  # noqa: F401  (shard_tiles needs the library)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    digests, cuts, slow = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    tiles, vals = _tiles()
+    assert cuts[0] == 0 and cuts[-1] == len(tiles) and cuts[0] < cuts[1] < cuts[2]
+    op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+    for i, tile in enumerate(tiles):
+        rc, out = op.unfilter_tile(tile, W.TILE_BYTES)
+        assert rc == 0
+        assert digests[i] == int(np.frombuffer(out, dtype=np.uint32).astype(np.uint64).sum()) + 1
+    assert slow == 2.0

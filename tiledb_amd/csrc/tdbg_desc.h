@@ -37,7 +37,8 @@ struct tdbg_plan {
   tdbg_stage s[TDBG_MAX_FILTERS];
 };
 
-#define TDBG_E_FALLBACK 100  // internal: fast path declined the tile
+#define TDBG_E_FALLBACK 100
+#define TDBG_PROF_PHASES 8  // fused-kernel phase clocks per workgroup  // internal: fast path declined the tile
 
 enum tdbg_fast_kind : uint32_t {
   TDBG_FAST_NONE = 0,
@@ -60,6 +61,7 @@ struct KParams {
   uint32_t slot_cap, md_cap, tab_cap;
   uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
   uint32_t fixup;     // general kernel: only tiles whose status is TDBG_E_FALLBACK
+  uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
   tdbg_plan plan;
 };
 

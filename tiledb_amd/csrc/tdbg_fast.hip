@@ -42,6 +42,8 @@ struct FastLds {
   uint64_t red[4 * FNT / 64 + 8];
   uint32_t flag[4];
   uint32_t pairs[3 * 16];  // compression part table: un, cn, input offset
+  uint64_t scan2[2][FNT / 64];  // one-barrier stage scans, ping-pong by stage position
+  uint32_t scanf[2][FNT / 64];
 };
 
 struct View {
@@ -79,6 +81,29 @@ __device__ __forceinline__ uint64_t ldsn(const uint8_t* X, uint32_t off, uint32_
   }
   const uint64_t v = lds64(X, off);
   return k == 8 ? v : (v & ((1ull << (8 * k)) - 1));
+}
+
+// Wave snapshot of 256 bytes of LDS: lane k holds bytes [4k, 4k + 4) of the
+// window.  Header fields at uniform offsets are then read with v_readlane
+// (scalar, no LDS round trip), so a parse is one LDS latency instead of a
+// chain of dependent ones.
+__device__ __forceinline__ uint32_t snap_take(const uint8_t* A, uint32_t base) {
+  return lds32(A, base + 4 * (tid_() & 63));
+}
+// o uniform, o + 4 <= 256
+__device__ __forceinline__ uint32_t snap32(uint32_t s, uint32_t o) {
+  const uint32_t d0 = __builtin_amdgcn_readlane(s, o >> 2);
+  if ((o & 3) == 0) return d0;
+  const uint32_t d1 = __builtin_amdgcn_readlane(s, (o >> 2) + 1);
+  return __builtin_amdgcn_alignbyte(d1, d0, o & 3);
+}
+__device__ __forceinline__ uint32_t snap8(uint32_t s, uint32_t o) {
+  return (__builtin_amdgcn_readlane(s, o >> 2) >> (8 * (o & 3))) & 0xffu;
+}
+// k in 1..8 bytes, o + 8 <= 256
+__device__ __forceinline__ uint64_t snapn(uint32_t s, uint32_t o, uint32_t k) {
+  const uint64_t v = (uint64_t)snap32(s, o) | ((uint64_t)snap32(s, o + 4) << 32);
+  return k >= 8 ? v : (v & ((1ull << (8 * k)) - 1));
 }
 
 // explicit global (address space 1) accesses: global_load/store, not flat
@@ -174,23 +199,29 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
     }
     return;
   }
-  // slice = whole units, >= 144 B so FNT slices cover XCAP
-  constexpr int SLB = UB >= 64 ? 192 : (UB == 32 ? 160 : 144);
-  constexpr int NU = SLB / UB;
-  constexpr int RD = SLB / 4;
-  uint32_t r[RD];
-  const uint32_t s0 = tid_() * SLB;
+  // in place: every unit of the stage is computed into registers (unit
+  // u = tid + k*FNT, lane-consecutive, so LDS reads and writes are
+  // conflict-free), barrier, then written back to X[0, n)
+  constexpr int NU = (XCAP + UB * FNT - 1) / (UB * FNT);
+  uint32_t r[NU * UD];
+  const uint32_t t = tid_();
 #pragma unroll
   for (int k = 0; k < NU; k++) {
-    const uint32_t u = tid_() * NU + k;
+    const uint32_t u = t + k * FNT;
     if (u * UB < n) fn(u, *(uint32_t(*)[UD])(r + k * UD));
     __builtin_amdgcn_sched_barrier(0);  // keep each unit's loads local
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < RD / 4; k++) {
-    const uint32_t o = s0 + 16 * k;
-    if (o < n) *(uint4*)(L.X + o) = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+  for (int k = 0; k < NU; k++) {
+    const uint32_t u = t + k * FNT;
+#pragma unroll
+    for (int q = 0; q < UD / 4; q++) {
+      const uint32_t o = u * UB + 16 * q;
+      if (o < n)
+        *(uint4*)(L.X + o) = make_uint4(r[k * UD + 4 * q], r[k * UD + 4 * q + 1], r[k * UD + 4 * q + 2],
+                                        r[k * UD + 4 * q + 3]);
+    }
   }
   __syncthreads();
 }
@@ -240,6 +271,7 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
   const uint8_t* X = L.X;
   if (TS == 1) {
     if (final) final_copy(L, cur, gout);
+    else __syncthreads();  // md reads done before a later stage rewrites MD
     return true;
   }
   const uint32_t full = (N * TS) & ~15u;  // bytes covered by whole vector units
@@ -331,6 +363,7 @@ __device__ __forceinline__ bool f_bitshuffle(FastLds& L, View& cur, uint32_t& mo
   const uint32_t n = ps, base = cur.base;
   if (n % TS != 0 || n % 8 != 0) {  // part copied, not shuffled
     if (final) final_copy(L, cur, gout);
+    else __syncthreads();  // md reads done before a later stage rewrites MD
     return true;
   }
   const uint8_t* X = L.X;
@@ -390,7 +423,7 @@ __device__ __forceinline__ uint64_t bwr_elem(const uint8_t* X, uint32_t base, ui
 
 template <int W, bool SGN>
 __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
-                      uint8_t* gout, uint32_t cap, uint32_t dts) {
+                      uint8_t* gout, uint32_t cap, uint32_t dts, uint32_t pos) {
   const uint32_t tid = tid_();
   if (mn < 8) return false;
   const uint32_t orig = lds32(L.MD, mo), nw = lds32(L.MD, mo + 4);
@@ -399,6 +432,32 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
   if (final ? orig > cap : orig > XCAP) return false;
   const uint32_t ws0 = lds32(L.MD, mo + 8 + dts + 1);
   bool bad = ws0 == 0 || ws0 % W != 0;
+  {
+    // Wave-local identity test (no barrier): every wave checks all windows.
+    // All windows raw with the uniform window layout <=> each window is
+    // copied to its own offset, and the stage is the identity on the first
+    // orig bytes (the common case for incompressible data).
+    const uint32_t lane = tid & 63;
+    bool nonraw = false, badl = false;
+    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
+      const uint32_t w = w0 + lane;
+      if (w < nw) {
+        const uint32_t eo = mo + 8 + w * E;
+        const uint32_t bits = L.MD[eo + dts], nbw = lds32(L.MD, eo + dts + 1);
+        nonraw |= !(bits >= 8u * W || (nbw % W) != 0);
+        badl |= w + 1 < nw ? nbw != ws0 : (nbw == 0 || nbw > ws0);
+      }
+    }
+    if (!bad && __ballot(nonraw) == 0 && __ballot(badl) == 0) {
+      const uint64_t tot = (uint64_t)(nw - 1) * ws0 + lds32(L.MD, mo + 8 + (nw - 1) * E + dts + 1);
+      if (tot != orig || tot > cur.n) return false;
+      mo += 8 + nw * E;
+      mn -= 8 + nw * E;
+      cur.n = orig;
+      if (final) final_copy(L, cur, gout);
+      return true;
+    }
+  }
   uint32_t comp = 0, nb = 0;
   uint4 ent = make_uint4(0, 0, 0, 0);
   if (tid < nw) {
@@ -410,20 +469,45 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     comp = raw ? nb : (nb / W) * (bits >> 3);
     if (!raw && bits != 8 && bits != 16 && bits != 32) bad = true;
     if (tid + 1 < nw ? nb != ws0 : (nb == 0 || nb > ws0)) bad = true;
+    if (nb > XCAP) bad = true;  // keeps the packed sums below 2^32
     ent = make_uint4(0, bits | (raw ? 0x100u : 0u), (uint32_t)off, (uint32_t)(off >> 32));
   }
-  uint64_t tin;
-  const uint32_t in_off = (uint32_t)block_exscan_u64<FNT>(comp, tin, L.red);
-  uint64_t tout;
-  block_exscan_u64<FNT>(nb, tout, L.red);
+  // one scan of (comp, nb) packed in a u64 (both sums < 2^32), with the
+  // 'bad' and 'not raw' flags OR-ed alongside: a single barrier.  Every
+  // window raw <=> in_off == tid * ws0 (non-last windows hold ws0 bytes), in
+  // which case the stage is the identity on the first orig bytes.
+  const uint32_t lane = tid & 63, wid = tid >> 6;
+  const uint64_t packed = ((uint64_t)comp << 32) | nb;
+  const uint64_t inc = wave_incscan_u64(packed);
+  const bool badw = __ballot(bad) != 0;
+  const bool cmpw = __ballot(tid < nw && !(ent.y & 0x100u)) != 0;
+  if (lane == 63) L.scan2[pos & 1][wid] = inc;
+  if (lane == 0) L.scanf[pos & 1][wid] = (badw ? 1u : 0u) | (cmpw ? 2u : 0u);
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  uint32_t fl = 0;
+#pragma unroll
+  for (int i = 0; i < FNT / 64; i++) {
+    const uint64_t s = L.scan2[pos & 1][i];
+    if ((uint32_t)i < wid) pre += s;
+    tot += s;
+    fl |= L.scanf[pos & 1][i];
+  }
+  const uint32_t in_off = (uint32_t)((pre + inc - packed) >> 32);
+  const uint64_t tin = tot >> 32, tout = tot & 0xffffffffu;
+  if ((fl & 1u) || tin > cur.n || tout != orig) return false;
+  mo += 8 + nw * E;
+  mn -= 8 + nw * E;
+  if (!(fl & 2u)) {
+    cur.n = orig;
+    if (final) final_copy(L, cur, gout);
+    return true;
+  }
   if (tid < nw) {
     ent.x = in_off;
     L.TAB[tid] = ent;
   }
-  bad = bad || tin > cur.n || tout != orig;
-  if (block_any(bad)) return false;
-  mo += 8 + nw * E;
-  mn -= 8 + nw * E;
+  __syncthreads();
   const uint8_t* X = L.X;
   const uint32_t base = cur.base;
   const bool pow2 = (ws0 & (ws0 - 1)) == 0;
@@ -664,30 +748,32 @@ __device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32
 // ---------------------------------------------------------------------------
 // serial codecs for tiny metadata parts (thread 0)
 // ---------------------------------------------------------------------------
-// DoubleDelta::decompress of one part into dst; false on any anomaly.
-__device__ bool dd_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32_t un, uint32_t W) {
+// DoubleDelta::decompress of one part (dd_compressor.cc:314-360); false on
+// any anomaly.  rd(o) returns source byte o, wr(o, v) stores output byte o.
+template <class R, class Wr>
+__device__ __forceinline__ bool dd_serial_g(R&& rd8, uint32_t cn, Wr&& wr8, uint32_t un, uint32_t W) {
   if (cn < 9) return false;
-  const uint32_t b = src[0];
+  const uint32_t b = rd8(0);
   uint64_t num = 0;
-  for (int i = 0; i < 8; i++) num |= (uint64_t)src[1 + i] << (8 * i);
+  for (int i = 0; i < 8; i++) num |= (uint64_t)rd8(1 + i) << (8 * i);
   if (b >= 8 * W - 1) {
     if (cn - 9 != un) return false;
-    for (uint32_t i = 0; i < un; i++) dst[i] = src[9 + i];
+    for (uint32_t i = 0; i < un; i++) wr8(i, rd8(9 + i));
     return true;
   }
   if (num * W != un || num == 0) return false;
   auto rd = [&](uint32_t off, uint32_t k) {
     uint64_t v = 0;
-    for (uint32_t i = 0; i < k; i++) v |= (uint64_t)src[off + i] << (8 * i);
+    for (uint32_t i = 0; i < k; i++) v |= (uint64_t)rd8(off + i) << (8 * i);
     return v;
   };
   if (cn < 9 + W) return false;
   uint64_t x0 = rd(9, W);
-  for (uint32_t i = 0; i < W; i++) dst[i] = (uint8_t)(x0 >> (8 * i));
+  for (uint32_t i = 0; i < W; i++) wr8(i, (uint8_t)(x0 >> (8 * i)));
   if (num == 1) return true;
   if (cn < 9 + 2 * W) return false;
   uint64_t x1 = rd(9 + W, W);
-  for (uint32_t i = 0; i < W; i++) dst[W + i] = (uint8_t)(x1 >> (8 * i));
+  for (uint32_t i = 0; i < W; i++) wr8(W + i, (uint8_t)(x1 >> (8 * i)));
   if (num == 2) return true;
   const uint64_t words = ((num - 2) * (b + 1) + 63) / 64;
   if (9 + 2 * W + 8 * words > cn) return false;
@@ -704,9 +790,14 @@ __device__ bool dd_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32_
     const uint64_t e = ((code >> b) & 1) ? (0 - mag) : mag;
     d += e;
     x += d;
-    for (uint32_t k = 0; k < W; k++) dst[i * W + k] = (uint8_t)(x >> (8 * k));
+    for (uint32_t k = 0; k < W; k++) wr8(i * W + k, (uint8_t)(x >> (8 * k)));
   }
   return true;
+}
+
+__device__ bool dd_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32_t un, uint32_t W) {
+  return dd_serial_g([&](uint32_t o) -> uint32_t { return src[o]; }, cn,
+                     [&](uint32_t o, uint8_t v) { dst[o] = v; }, un, W);
 }
 
 __device__ bool rle_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32_t un, uint32_t cs) {
@@ -865,43 +956,76 @@ __device__ bool comp_header(FastLds& L, View cur, uint32_t mo, uint32_t mn, uint
 template <int W>
 __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap) {
-  uint32_t nmd, src, c, u, mdt;
-  if (!comp_header(L, cur, mo, mn, nmd, src, c, u, mdt)) return false;
+  // compression md header (compression_filter.cc:323-347) from a wave
+  // snapshot of MD; part table: (un, cn) pairs, md parts first
+  if (mn < 8) return false;
+  const uint32_t sm = snap_take(L.MD, mo);
+  const uint32_t sx = snap_take(L.X, cur.base);
+  const uint32_t nmd = snap32(sm, 0), nd = snap32(sm, 4);
+  if (nd != 1 || nmd > 15 || 8 + 8 * (nmd + 1) > mn) return false;
+  uint32_t p = 0, mdt = 0, src = 0, c = 0, u = 0;
+  for (uint32_t i = 0; i <= nmd; i++) {
+    const uint32_t un = snap32(sm, 8 + 8 * i), cn = snap32(sm, 12 + 8 * i);
+    if (i < nmd) mdt += un;
+    src = p;
+    c = cn;
+    u = un;
+    p += cn;
+  }
+  if (p > cur.n || mdt > MDCAP) return false;
   if (c < 9) return false;
-  const uint32_t b = L.X[src];
-  const uint64_t num = ldsn(L.X, src + 1, 8);
+  const bool in_snap = src + 9 + 8 <= 256;  // md parts and the data header in the snapshot
+  const uint32_t b = in_snap ? snap8(sx, src) : L.X[cur.base + src];
+  const uint64_t num = in_snap ? snapn(sx, src + 1, 8) : ldsn(L.X, cur.base + src + 1, 8);
   const bool raw = b >= 8u * W - 1;
-  bool bad = false;
-  if (final && u > cap) bad = true;
+  if (final && u > cap) return false;
   if (raw) {
-    if (c - 9 != u) bad = true;
+    if (c - 9 != u) return false;
   } else {
-    if (num < 3 || num * W != u || u > (uint32_t)(FNT * SP) || dd_check(c, u, W, b, num)) bad = true;
+    if (num < 3 || num * W != u || u > (uint32_t)(FNT * SP) || dd_check(c, u, W, b, num)) return false;
   }
-  if (bad) return false;
-  // metadata parts: thread 0, serially, into MD[0, mdt)
-  __syncthreads();  // every thread has read the header
-  if (tid_() == 0) {
+  // metadata parts, serially, into MD[0, mdt).  When that range lies below
+  // the compression header and the parts are in the snapshot (the usual
+  // case), every wave decodes them from its registers and its lane 0 writes
+  // them (identical bytes from every wave; no barrier).  Otherwise thread 0
+  // decodes from LDS between two barriers.
+  if (mo >= mdt && in_snap) {
+    const bool l0 = (tid_() & 63) == 0;
     bool ok = true;
-    uint32_t o = 0;
-    for (uint32_t i = 0; i < nmd; i++) {
-      const uint32_t un = L.pairs[3 * i], cn = L.pairs[3 * i + 1], ip = L.pairs[3 * i + 2];
-      ok = ok && dd_serial(L.X + cur.base + ip, cn, L.MD + o, un, W);
+    uint32_t o = 0, ip = 0;
+    for (uint32_t i = 0; i < nmd && ok; i++) {
+      const uint32_t un = snap32(sm, 8 + 8 * i), cn = snap32(sm, 12 + 8 * i);
+      ok = dd_serial_g([&](uint32_t q) -> uint32_t { return snap8(sx, ip + q); }, cn,
+                       [&](uint32_t q, uint8_t v) { if (l0) L.MD[o + q] = v; }, un, W);
       o += un;
+      ip += cn;
     }
-    L.flag[0] = ok ? 0u : 1u;
+    if (!ok) return false;
+  } else {
+    __syncthreads();  // every thread has read the header
+    if (tid_() == 0) {
+      bool ok = true;
+      uint32_t o = 0, ip = 0;
+      for (uint32_t i = 0; i < nmd; i++) {
+        const uint32_t un = lds32(L.MD, mo + 8 + 8 * i), cn = lds32(L.MD, mo + 12 + 8 * i);
+        ok = ok && dd_serial(L.X + cur.base + ip, cn, L.MD + o, un, W);
+        o += un;
+        ip += cn;
+      }
+      L.flag[0] = ok ? 0u : 1u;
+    }
+    __syncthreads();
+    if (L.flag[0]) return false;
   }
-  __syncthreads();
-  if (L.flag[0]) return false;
   mo = 0;
   mn = mdt;
   if (raw) {
-    cur.base = src + 9;
+    cur.base = cur.base + src + 9;
     cur.n = u;
     if (final) final_copy(L, cur, gout);
     return true;
   }
-  dd_decode_part<W>(L, src, b, num);
+  dd_decode_part<W>(L, cur.base + src, b, num);
   cur.base = 0;
   cur.n = u;
   if (final) final_copy(L, cur, gout);
@@ -981,7 +1105,7 @@ __device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint3
 // inference see one small straight-line program.
 #define SC(kind, w, sg) ((kind) | ((w) << 4) | ((sg) << 8))
 
-template <int CODE>
+template <int CODE, int POS>
 __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn,
                                           bool final, uint8_t* gout, uint32_t cap,
                                           const tdbg_stage& s) {
@@ -998,7 +1122,7 @@ __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, u
   } else if constexpr (K == TDBG_K_BITSHUFFLE) {
     return f_bitshuffle<W>(L, cur, mo, mn, final, gout, cap);
   } else if constexpr (K == TDBG_K_BWR) {
-    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts);
+    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts, POS);
   } else if constexpr (K == TDBG_K_PD) {
     return f_pd<W>(L, cur, mo, mn, final, gout, cap, s.dts);
   } else if constexpr (K == TDBG_K_DD) {
@@ -1010,8 +1134,66 @@ __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, u
   }
 }
 
-// Returns true when the chunk was fully unfiltered into gout; false = the
-// general interpreter must redo the tile (nothing was written to gout).
+// Runs the pipeline on a chunk already staged in LDS (data view `cur`,
+// metadata at L.MD[mo, mo+mn)).  `hook` runs right before the final stage,
+// which only reads LDS and streams to HBM: the caller issues the next tile's
+// loads there.  Returns true when gout holds the unfiltered chunk; false =
+// the general interpreter must redo the tile (nothing was written to gout).
+// Diagnostics: per-workgroup accumulated shader-clock cycles per phase
+// (0 wait for the tile, 1 headers, 2-4 intermediate stages in run order,
+// 5 final stage, 6 loop tail), enabled by KParams::prof.
+struct PhaseClock {
+  uint64_t* out;
+  uint64_t t, acc[TDBG_PROF_PHASES];
+  __device__ __forceinline__ void init(uint64_t* o) {
+    out = o;
+    if (!out) return;
+    t = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < TDBG_PROF_PHASES; k++) acc[k] = 0;
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (!out) return;
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    acc[k] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void flush() {
+    if (!out || tid_() != 0) return;
+    for (int k = 0; k < TDBG_PROF_PHASES; k++) out[blockIdx.x * TDBG_PROF_PHASES + k] = acc[k];
+  }
+};
+
+template <int S0, int S1, int S2, int S3, class H, class M>
+__device__ __forceinline__ bool f_resident(const tdbg_plan& P, View cur, uint32_t mo, uint32_t mn,
+                                           uint8_t* gout, uint32_t orig, FastLds& L,
+                                           uint32_t dbg_stop, H&& hook, M&& mark) {
+  if (dbg_stop == 1) return true;  // timing ablation: load only
+  // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
+  if constexpr (S3 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
+    if (!run_stage<S3, 3>(L, cur, mo, mn, false, gout, orig, P.s[3])) return false;
+    if (cur.n > XCAP) return false;
+    mark(2);
+  }
+  if constexpr (S2 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
+    if (!run_stage<S2, 2>(L, cur, mo, mn, false, gout, orig, P.s[2])) return false;
+    if (cur.n > XCAP) return false;
+    mark(S3 != 0 ? 3 : 2);
+  }
+  if constexpr (S1 != 0) {
+    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
+    if (!run_stage<S1, 1>(L, cur, mo, mn, false, gout, orig, P.s[1])) return false;
+    if (cur.n > XCAP) return false;
+    mark(S3 != 0 ? 4 : S2 != 0 ? 3 : 2);
+  }
+  if (dbg_stop > 1) return true;
+  hook();
+  const bool ok = run_stage<S0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0]);
+  mark(5);
+  return ok;
+}
+
 template <int S0, int S1, int S2, int S3>
 __device__ __forceinline__ bool f_chunk(const tdbg_plan& P, const uint8_t* gmd, uint32_t ml,
                                         const uint8_t* gdata, uint32_t fl, uint8_t* gout,
@@ -1022,39 +1204,145 @@ __device__ __forceinline__ bool f_chunk(const tdbg_plan& P, const uint8_t* gmd, 
   const bool ok_m = load_to_lds(L.MD, MDCAP, gmd, ml, &mbase);
   if (!ok_d || !ok_m) return false;
   __syncthreads();
-  View cur = {dbase, fl};
-  uint32_t mo = mbase, mn = ml;
-  if (dbg_stop == 1) return true;  // timing ablation: load only
-  // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
-  if constexpr (S3 != 0) {
-    if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
-    if (!run_stage<S3>(L, cur, mo, mn, false, gout, orig, P.s[3])) return false;
-    if (cur.n > XCAP) return false;
+  return f_resident<S0, S1, S2, S3>(P, View{dbase, fl}, mbase, ml, gout, orig, L, dbg_stop,
+                                    [] {}, [](int) {});
+}
+
+// Whole-tile prefetch: the filtered tile image (tile header, chunk header,
+// metadata, data) is one contiguous range whose size the host knows, so its
+// loads can be issued a tile ahead into registers and committed to LDS later.
+constexpr int PLU = (XCAP / 16 + FNT - 1) / FNT;
+constexpr uint32_t PCAP = PLU * FNT * 16;  // bytes of tile image the registers hold
+// The prefetch keeps PLU*4 VGPRs live through the final stage; specs whose
+// final stage is a scan (PD, DD) or that decode 8-byte DD would spill.
+constexpr bool pf_enabled(int s0, int s1, int s2, int s3) {
+  return (s0 & 15) != TDBG_K_PD && (s0 & 15) != TDBG_K_DD &&
+         s1 != (TDBG_K_DD | 8 << 4) && s2 != (TDBG_K_DD | 8 << 4) && s3 != (TDBG_K_DD | 8 << 4);
+}
+
+struct Pref {
+  v4u v[PLU];
+  uint32_t h;  // lane k of every wave: dword k of the image's first 64 bytes
+  uint32_t cnt, base;
+  bool ok;
+};
+
+__device__ __forceinline__ void pf_issue(Pref& pf, const uint8_t* g, uint64_t n) {
+  const uintptr_t a0 = (uintptr_t)g & ~(uintptr_t)15;
+  const uintptr_t a1 = ((uintptr_t)g + n + 15) & ~(uintptr_t)15;
+  pf.cnt = (uint32_t)((a1 - a0) >> 4);
+  pf.base = (uint32_t)((uintptr_t)g - a0);
+  pf.ok = n >= 20 && n <= PCAP && (uint64_t)pf.cnt * 16 <= PCAP;
+  if (!pf.ok) return;
+  const g_cu4* src = (const g_cu4*)a0;
+  const uint32_t t = tid_();
+  const uint32_t hd = (t & 63) < 4 * pf.cnt ? (t & 63) : 4 * pf.cnt - 1;
+  pf.h = ((const g_cu32*)a0)[hd];
+#pragma unroll
+  for (int k = 0; k < PLU; k++) {
+    const uint32_t u = t + k * FNT;
+    pf.v[k] = src[u < pf.cnt ? u : pf.cnt - 1];
   }
-  if constexpr (S2 != 0) {
-    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S2>(L, cur, mo, mn, false, gout, orig, P.s[2])) return false;
-    if (cur.n > XCAP) return false;
+}
+
+// The registers are consumed: tell the compiler, so they are not kept live
+// through code that does not use them (the loads were issued long ago).
+__device__ __forceinline__ void pf_kill(Pref& pf) {
+#pragma unroll
+  for (int k = 0; k < PLU; k++) pf.v[k] = v4u{0u, 0u, 0u, 0u};
+}
+
+// Commit: metadata bytes [m, m + ml) of the image go to L.MD and
+// data bytes [m + ml, m + ml + fl) to L.X, each shifted by a whole number of
+// 16-B units (so md starts at MD[m & 15], data at X[(m + ml) & 15]).
+__device__ __forceinline__ void pf_commit_split(const Pref& pf, FastLds& L, uint32_t m, uint32_t ml) {
+  const uint32_t t = tid_();
+  const uint32_t m0 = m & ~15u, d = m + ml, d0 = d & ~15u;
+#pragma unroll
+  for (int k = 0; k < PLU; k++) {
+    const uint32_t u = t + k * FNT, o = 16 * u;
+    if (u < pf.cnt) {
+      if (o + 16 > m && o < d) *(v4u*)(L.MD + (o - m0)) = pf.v[k];
+      if (o + 16 > d) *(v4u*)(L.X + (o - d0)) = pf.v[k];
+    }
   }
-  if constexpr (S1 != 0) {
-    if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S1>(L, cur, mo, mn, false, gout, orig, P.s[1])) return false;
-    if (cur.n > XCAP) return false;
-  }
-  if (dbg_stop > 1) return true;
-  return run_stage<S0>(L, cur, mo, mn, true, gout, orig, P.s[0]);
+}
+
+// A tile's batch entry.  Loaded a tile ahead with vector loads (an opaque
+// zero offset keeps them off the scalar unit: scalar loads share lgkmcnt with
+// every LDS access, so the first LDS wait after them would stall on HBM).
+struct TileDesc {
+  uint64_t t, fs, os;
+  const uint8_t* in;
+  uint8_t* out;
+};
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ TileDesc desc_load(const KParams& kp, uint64_t j) {
+  uint32_t z = 0;
+  asm volatile("" : "+v"(z));
+  TileDesc d;
+  d.t = kp.tile_list ? kp.tile_list[j + z] : j + z;
+  d.fs = kp.in_size[d.t + z];
+  d.os = kp.out_size[d.t + z];
+  d.in = kp.in[d.t + z];
+  d.out = kp.out[d.t + z];
+  return d;
+}
+
+__device__ __forceinline__ TileDesc desc_uniform(const TileDesc& d) {
+  TileDesc u;
+  u.t = uni64(d.t);
+  u.fs = uni64(d.fs);
+  u.os = uni64(d.os);
+  u.in = (const uint8_t*)uni64((uint64_t)d.in);
+  u.out = (uint8_t*)uni64((uint64_t)d.out);
+  return u;
 }
 
 template <int S0, int S1, int S2, int S3>
 __global__ void __launch_bounds__(FNT, 4)
 unfilter_fused_kernel(const KParams kp) {
   __shared__ FastLds L;
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
-    const uint64_t t = kp.tile_list ? kp.tile_list[j] : j;
-    const uint8_t* in = kp.in[t];
-    const uint64_t fs = kp.in_size[t];
-    uint8_t* out = kp.out[t];
-    const uint64_t os = kp.out_size[t];
+  const uint64_t G = gridDim.x;
+  PhaseClock pc;
+  pc.init(kp.prof);
+  Pref pf;
+  pf.ok = false;
+  pf.cnt = 0;
+  pf.base = 0;
+  constexpr bool PF = pf_enabled(S0, S1, S2, S3);
+  TileDesc dn{};
+  if (blockIdx.x < kp.ntiles) {
+    dn = desc_uniform(desc_load(kp, blockIdx.x));
+    if (PF) pf_issue(pf, dn.in, dn.fs);
+  }
+  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += G) {
+    const TileDesc d = dn;
+    const uint64_t t = d.t;
+    const uint8_t* in = d.in;
+    const uint64_t fs = d.fs;
+    uint8_t* out = d.out;
+    const uint64_t os = d.os;
+    const uint64_t jn = j + G;
+    TileDesc dl{};
+    if (jn < kp.ntiles) dl = desc_load(kp, jn);  // consumed by the hook
+    bool hooked = false;
+    auto hook = [&]() {
+      hooked = true;
+      if (jn < kp.ntiles) {
+        dn = desc_uniform(dl);
+        if (PF) pf_issue(pf, dn.in, dn.fs);
+      } else {
+        pf.ok = false;
+        pf_kill(pf);
+      }
+    };
     int rc = TDBG_OK;
     // Tile::load_chunk_data (tile.cc:280-313)
     uint64_t expected = os;
@@ -1062,8 +1350,36 @@ unfilter_fused_kernel(const KParams kp) {
       if (os < 8) rc = TDBG_E_TILE_SIZE;
       expected = os - 8;
     }
-    uint64_t nch = 0;
-    if (rc == TDBG_OK) {
+    bool handled = false;
+    if (rc == TDBG_OK && pf.ok) {
+      // the whole tile is in registers; every wave reads the tile and chunk
+      // headers from its own copy of the first dwords (no LDS, no barrier),
+      // then metadata goes to L.MD and data to L.X (stages rewrite X in place)
+      const uint32_t b = pf.base;
+      const uint64_t nch = (uint64_t)snap32(pf.h, b) | ((uint64_t)snap32(pf.h, b + 4) << 32);
+      pc.mark(0);
+      if (nch == 1) {
+        handled = true;
+        const uint32_t orig = snap32(pf.h, b + 8), fl = snap32(pf.h, b + 12), ml = snap32(pf.h, b + 16);
+        if (ml > fs - 20 || fl > fs - 20 - ml) rc = TDBG_E_TILE_FORMAT;
+        else if (orig != expected) rc = TDBG_E_TILE_SIZE;
+        else if (ml + 32 > MDCAP || fl + 32 > XCAP) rc = TDBG_E_FALLBACK;
+        else {
+          const uint32_t m = b + 20;
+          pf_commit_split(pf, L, m, ml);
+          pf_kill(pf);
+          __syncthreads();
+          pc.mark(1);
+          const bool done = f_resident<S0, S1, S2, S3>(kp.plan, View{(m + ml) & 15u, fl}, m & 15u,
+                                                       ml, out, orig, L, kp.dbg_stop, hook,
+                                                       [&](int k) { pc.mark(k); });
+          if (!done) rc = TDBG_E_FALLBACK;
+        }
+      }
+    }
+    if (!handled && rc == TDBG_OK) {
+      pf_kill(pf);
+      uint64_t nch = 0;
       if (fs < 8) rc = TDBG_E_TILE_FORMAT;
       else {
         nch = gldn(in, 8);
@@ -1080,26 +1396,30 @@ unfilter_fused_kernel(const KParams kp) {
         }
         if (rc == TDBG_OK && total != expected) rc = TDBG_E_TILE_SIZE;
       }
-    }
-    if (rc == TDBG_OK) {
-      uint64_t o = 8, coff = 0;
-      for (uint64_t i = 0; i < nch; i++) {
-        const uint32_t orig = (uint32_t)gldn(in + o, 4), fl = (uint32_t)gldn(in + o + 4, 4),
-                       ml = (uint32_t)gldn(in + o + 8, 4);
-        o += 12;
-        const bool done = f_chunk<S0, S1, S2, S3>(kp.plan, in + o, ml, in + o + ml, fl, out + coff,
-                                                  orig, L, kp.dbg_stop);
-        __syncthreads();
-        if (!done) {  // the general fixup launch redoes the whole tile
-          rc = TDBG_E_FALLBACK;
-          break;
+      if (rc == TDBG_OK) {
+        uint64_t o = 8, coff = 0;
+        for (uint64_t i = 0; i < nch; i++) {
+          const uint32_t orig = (uint32_t)gldn(in + o, 4), fl = (uint32_t)gldn(in + o + 4, 4),
+                         ml = (uint32_t)gldn(in + o + 8, 4);
+          o += 12;
+          const bool done = f_chunk<S0, S1, S2, S3>(kp.plan, in + o, ml, in + o + ml, fl,
+                                                    out + coff, orig, L, kp.dbg_stop);
+          __syncthreads();
+          if (!done) {  // the general fixup launch redoes the whole tile
+            rc = TDBG_E_FALLBACK;
+            break;
+          }
+          o += ml + fl;
+          coff += orig;
         }
-        o += ml + fl;
-        coff += orig;
       }
     }
+    if (!hooked) hook();
+    __syncthreads();  // LDS reads of this tile done before the next commit
     if (tid_() == 0 && kp.status) kp.status[t] = rc;
+    pc.mark(6);
   }
+  pc.flush();
 }
 
 }  // namespace tdbg

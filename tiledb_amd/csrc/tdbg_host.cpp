@@ -121,6 +121,9 @@ struct tdbg_context {
     hipEvent_t h2d = nullptr, kdone = nullptr, done = nullptr;
   } st[2];
   hipStream_t cstream = nullptr;   // compute stream: kernels serialized (shared scratch)
+  // diagnostics (TDBG_PROF=1): fused-kernel phase clocks of the last launch
+  uint64_t* d_prof = nullptr;
+  uint32_t prof_grid = 0;
 };
 
 namespace {
@@ -396,6 +399,7 @@ void tdbg_context_destroy(tdbg_context* c) {
     if (s.done) (void)hipEventDestroy(s.done);
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->d_prof) (void)hipFree(c->d_prof);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -439,6 +443,20 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   kp.slot_cap = c->slot_cap;
   kp.md_cap = c->md_cap;
   kp.tab_cap = c->tab_cap;
+  {
+    static const bool prof = getenv("TDBG_PROF") != nullptr;
+    if (prof && fast) {
+      if (c->prof_grid < grid) {
+        if (c->d_prof) (void)hipFree(c->d_prof);
+        c->d_prof = nullptr;
+        c->prof_grid = 0;
+        HIP_OK(hipMalloc(&c->d_prof, sizeof(uint64_t) * TDBG_PROF_PHASES * grid));
+        c->prof_grid = grid;
+      }
+      HIP_OK(hipMemsetAsync(c->d_prof, 0, sizeof(uint64_t) * TDBG_PROF_PHASES * c->prof_grid, stream));
+      kp.prof = c->d_prof;
+    }
+  }
   HIP_OK(hipEventRecord(c->ev0, stream));
   hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
@@ -559,6 +577,19 @@ int tdbg_context_last_kernel_ms(tdbg_context* c, float* ms) {
   if (!c->timed) return fail(TDBG_E_ARG, "no kernel launched yet");
   HIP_OK(hipEventSynchronize(c->ev1));
   HIP_OK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return TDBG_OK;
+}
+
+int tdbg_debug_phase_clocks(tdbg_context* c, uint64_t* out, uint32_t nphases) {
+  if (!c || !out) return fail(TDBG_E_ARG, "null argument");
+  for (uint32_t k = 0; k < nphases; k++) out[k] = 0;
+  if (!c->d_prof) return fail(TDBG_E_ARG, "no profiled launch (set TDBG_PROF=1)");
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipDeviceSynchronize());
+  std::vector<uint64_t> h((size_t)TDBG_PROF_PHASES * c->prof_grid);
+  HIP_OK(hipMemcpy(h.data(), c->d_prof, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  for (uint32_t g = 0; g < c->prof_grid; g++)
+    for (uint32_t k = 0; k < nphases && k < TDBG_PROF_PHASES; k++) out[k] += h[(size_t)g * TDBG_PROF_PHASES + k];
   return TDBG_OK;
 }
 
@@ -729,6 +760,25 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   return TDBG_OK;
 }
 
+int tdbg_shard_tiles(uint64_t ntiles, const uint64_t* in_size, const uint64_t* out_size,
+                     uint32_t nshards, uint64_t* cuts) {
+  if (!cuts || nshards == 0 || (ntiles && (!in_size || !out_size)))
+    return fail(TDBG_E_ARG, "bad shard arguments");
+  // contiguous shards balanced by filtered + unfiltered bytes: shard k ends
+  // at the first tile where the running total reaches k/nshards of the whole
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < ntiles; i++) total += in_size[i] + out_size[i];
+  uint32_t k = 1;
+  uint64_t acc = 0;
+  cuts[0] = 0;
+  for (uint64_t i = 0; i < ntiles && k < nshards; i++) {
+    acc += in_size[i] + out_size[i];
+    while (k < nshards && (unsigned __int128)acc * nshards >= (unsigned __int128)total * k) cuts[k++] = i + 1;
+  }
+  while (k <= nshards) cuts[k++] = ntiles;
+  return TDBG_OK;
+}
+
 int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   const uint8_t* const* in, const uint64_t* in_size,
                                   uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
@@ -736,17 +786,8 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   uint64_t batch_bytes) {
   if (!p || !devices || ndev <= 0) return fail(TDBG_E_ARG, "bad device list");
   if (ntiles == 0) return TDBG_OK;
-  // contiguous shards balanced by filtered + unfiltered bytes
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < ntiles; i++) total += in_size[i] + out_size[i];
-  std::vector<uint64_t> cut{0};
-  uint64_t acc = 0;
-  for (uint64_t i = 0; i < ntiles && (int)cut.size() < ndev; i++) {
-    acc += in_size[i] + out_size[i];
-    if (acc * ndev >= total * cut.size()) cut.push_back(i + 1);
-  }
-  while ((int)cut.size() <= ndev) cut.push_back(ntiles);
-  cut[ndev] = ntiles;
+  std::vector<uint64_t> cut(ndev + 1);
+  tdbg_shard_tiles(ntiles, in_size, out_size, (uint32_t)ndev, cut.data());
   std::vector<int> rcs(ndev, 0);
   std::vector<std::string> errs(ndev);
   std::vector<int32_t> st(ntiles, 0);

@@ -186,6 +186,13 @@ class Context:
         _check(lib.tdbg_context_last_kernel_ms(self.h, ctypes.byref(ms)), "last_kernel_ms")
         return float(ms.value)
 
+    def phase_clocks(self, nphases: int = 8) -> np.ndarray:
+        """Diagnostics: fused-kernel cycles per phase of the last launch (TDBG_PROF=1)."""
+        out = np.zeros(nphases, dtype=np.uint64)
+        _check(lib.tdbg_debug_phase_clocks(
+            self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nphases), "phase_clocks")
+        return out
+
     def unfilter_host(self, dp: DevicePipeline, in_ptrs: np.ndarray, in_size: np.ndarray,
                       out_ptrs: np.ndarray, out_size: np.ndarray, offsets_tiles: bool = False,
                       batch_bytes: int = 0) -> np.ndarray:
@@ -221,6 +228,21 @@ def unfilter_multi_gpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size,
     if rc and not st[:n].any():
         _check(rc, "tdbg_unfilter_tiles_multi_gpu")
     return st[:n]
+
+
+def shard_tiles(in_size, out_size, nshards: int) -> np.ndarray:
+    """Contiguous shard boundaries (nshards + 1 tile indices), byte-balanced.
+
+    Rank r of a one-process-per-GPU job unfilters tiles [cuts[r], cuts[r+1]);
+    the same cut drives tdbg_unfilter_tiles_multi_gpu."""
+    isz = np.ascontiguousarray(in_size, dtype=np.uint64)
+    osz = np.ascontiguousarray(out_size, dtype=np.uint64)
+    if isz.size != osz.size:
+        raise ValueError("in_size and out_size differ in length")
+    cuts = np.zeros(nshards + 1, dtype=np.uint64)
+    _check(lib.tdbg_shard_tiles(isz.size, isz.ctypes.data, osz.ctypes.data, nshards,
+                                cuts.ctypes.data), "tdbg_shard_tiles")
+    return cuts
 
 
 def device_count() -> int:

@@ -1,0 +1,27 @@
+"""Per-phase cycle breakdown of the fused kernel on the C5 bench workload.
+Run on the GPU box:  TDBG_PROF=1 python tools/phase_prof.py"""
+import os, sys
+os.environ.setdefault("TDBG_PROF", "1")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import bench
+import workloads as W
+from tiledb_amd import engine
+
+NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c", "final", "tail", "-"]
+dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+ctx = engine.Context(0)
+for var in sys.argv[1:] or ["rand", "ramp"]:
+    batch = bench.build_batch(engine, var, 12500, 128, 0, seed=5)[0]
+    for _ in range(3):
+        ctx.unfilter_async(dp, batch)
+    torch.cuda.synchronize()
+    ms = ctx.last_kernel_ms()
+    clk = ctx.phase_clocks().astype(np.float64)
+    tot = clk.sum()
+    print(f"{var}: launch {ms:.4f} ms; per-WG phase share:",
+          ", ".join(f"{n} {100 * c / tot:.1f}%" for n, c in zip(NAMES, clk) if c), flush=True)
+    del batch
+    torch.cuda.empty_cache()
