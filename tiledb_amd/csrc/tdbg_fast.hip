@@ -63,12 +63,17 @@ __device__ __forceinline__ uint32_t tid_() {
 // ---------------------------------------------------------------------------
 // LDS byte access at arbitrary offsets (aligned dword reads + alignbyte)
 // ---------------------------------------------------------------------------
+// Branch-free: both dwords (one ds_read2_b32) and alignbyte, so reads batch.
 __device__ __forceinline__ uint32_t lds32(const uint8_t* X, uint32_t off) {
   const uint32_t a = off & ~3u, sh = off & 3u;
   const uint32_t lo = *(const uint32_t*)(X + a);
-  if (sh == 0) return lo;
   const uint32_t hi = *(const uint32_t*)(X + a + 4);
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+// the two dwords covering bytes [off, off + 4)
+__device__ __forceinline__ uint2 lds_pair(const uint8_t* X, uint32_t off) {
+  const uint32_t a = off & ~3u;
+  return make_uint2(*(const uint32_t*)(X + a), *(const uint32_t*)(X + a + 4));
 }
 __device__ __forceinline__ uint64_t lds64(const uint8_t* X, uint32_t off) {
   return (uint64_t)lds32(X, off) | ((uint64_t)lds32(X, off + 4) << 32);
@@ -185,14 +190,50 @@ __device__ __forceinline__ void store_unit(uint8_t* gout, uint32_t n, uint32_t o
 // ---------------------------------------------------------------------------
 // UB-byte units, computed by fn(u, w[UB/4]).  final: streamed to gout;
 // otherwise gathered per thread slice, barrier, written to X[0, n).
-template <int UB, class F>
-__device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_t* gout, F fn) {
+// Units [0, nfast) may use ffast, a branch-free variant that is safe for
+// any unit index below nfast: those are computed in rounds of RU units with
+// clamped indices (every LDS read of a round issued back to back, no
+// per-unit control flow); the remaining units use fany.
+template <int UB, class FF, class FA>
+__device__ __forceinline__ void drive2(FastLds& L, uint32_t n, uint32_t nfast, bool final, uint8_t* gout,
+                                       FF ffast, FA fany) {
   constexpr int UD = UB / 4;
+  constexpr int RU = UB == 16 ? 3 : 1;
+  const uint32_t t = tid_();
   if (final) {
     const uint32_t nu = (n + UB - 1) / UB;
-    for (uint32_t u = tid_(); u < nu; u += FNT) {
+    uint32_t done = 0;
+    if ((((uintptr_t)gout) & 15) == 0 && nfast > 0) {  // uniform
+      for (uint32_t u0 = 0; u0 < nfast; u0 += RU * FNT) {
+        uint32_t w[RU][UD];
+#pragma unroll
+        for (int r = 0; r < RU; r++) {
+          const uint32_t u = u0 + r * FNT + t;
+          ffast(u < nfast ? u : nfast - 1, w[r]);
+        }
+        // materialize every unit here: otherwise the compiler sinks a unit's
+        // LDS reads into its (predicated) store block and serializes them
+#pragma unroll
+        for (int r = 0; r < RU; r++)
+#pragma unroll
+          for (int q = 0; q < UD; q++) asm volatile("" : "+v"(w[r][q]));
+#pragma unroll
+        for (int r = 0; r < RU; r++) {
+          const uint32_t u = u0 + r * FNT + t;
+          if (u < nfast) {
+#pragma unroll
+            for (int q = 0; q < UD / 4; q++) {
+              v4u x = {w[r][4 * q], w[r][4 * q + 1], w[r][4 * q + 2], w[r][4 * q + 3]};
+              *(g_u4*)(gout + u * UB + 16 * q) = x;
+            }
+          }
+        }
+      }
+      done = nfast;
+    }
+    for (uint32_t u = done + t; u < nu; u += FNT) {
       uint32_t w[UD];
-      fn(u, w);
+      fany(u, w);
 #pragma unroll
       for (int q = 0; q < UD / 4; q++)
         store_unit(gout, n, u * UB + 16 * q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
@@ -204,12 +245,12 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
   // conflict-free), barrier, then written back to X[0, n)
   constexpr int NU = (XCAP + UB * FNT - 1) / (UB * FNT);
   uint32_t r[NU * UD];
-  const uint32_t t = tid_();
 #pragma unroll
   for (int k = 0; k < NU; k++) {
     const uint32_t u = t + k * FNT;
-    if (u * UB < n) fn(u, *(uint32_t(*)[UD])(r + k * UD));
-    __builtin_amdgcn_sched_barrier(0);  // keep each unit's loads local
+    if (u < nfast) ffast(u, *(uint32_t(*)[UD])(r + k * UD));
+    else if (u * UB < n) fany(u, *(uint32_t(*)[UD])(r + k * UD));
+    if (k % RU == RU - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
   }
   __syncthreads();
 #pragma unroll
@@ -224,6 +265,11 @@ __device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_
     }
   }
   __syncthreads();
+}
+
+template <int UB, class F>
+__device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_t* gout, F fn) {
+  drive2<UB>(L, n, 0, final, gout, fn, fn);
 }
 
 // Copy a view to the final output (pass-through / raw stages as filter 0).
@@ -285,58 +331,67 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
     }
   };
   if (TS == 4) {
-    drive<16>(L, n, final, gout, [&](uint32_t u, uint32_t (&w)[4]) {
-      if (16 * u + 16 <= full) {
-        const uint32_t i = 4 * u;
-        const uint32_t p0 = lds32(X, base + i), p1 = lds32(X, base + N + i);
-        const uint32_t p2 = lds32(X, base + 2 * N + i), p3 = lds32(X, base + 3 * N + i);
-        const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
-        const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
-        const uint32_t c = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
-        const uint32_t d = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
-        w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
-        w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
-        w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
-        w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
-      } else {
-        slow(u, w);
-      }
+    auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
+      const uint32_t i = 4 * u;
+      // the four plane reads issued together, aligned afterwards
+      const uint32_t o0 = base + i, o1 = o0 + N, o2 = o1 + N, o3 = o2 + N;
+      const uint2 r0 = lds_pair(X, o0), r1 = lds_pair(X, o1), r2 = lds_pair(X, o2), r3 = lds_pair(X, o3);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t p0 = __builtin_amdgcn_alignbyte(r0.y, r0.x, o0 & 3);
+      const uint32_t p1 = __builtin_amdgcn_alignbyte(r1.y, r1.x, o1 & 3);
+      const uint32_t p2 = __builtin_amdgcn_alignbyte(r2.y, r2.x, o2 & 3);
+      const uint32_t p3 = __builtin_amdgcn_alignbyte(r3.y, r3.x, o3 & 3);
+      const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
+      const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
+      const uint32_t c = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+      const uint32_t d = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+      w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+      w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+      w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
+    };
+    drive2<16>(L, n, full / 16, final, gout, fast, [&](uint32_t u, uint32_t (&w)[4]) {
+      if (16 * u + 16 <= full) fast(u, w);
+      else slow(u, w);
     });
   } else if (TS == 2) {
-    drive<16>(L, n, final, gout, [&](uint32_t u, uint32_t (&w)[4]) {
-      if (16 * u + 16 <= full) {
-        const uint32_t i = 8 * u;
-        const uint64_t p0 = lds64(X, base + i), p1 = lds64(X, base + N + i);
-        const uint32_t a0 = (uint32_t)p0, a1 = (uint32_t)(p0 >> 32);
-        const uint32_t b0 = (uint32_t)p1, b1 = (uint32_t)(p1 >> 32);
-        w[0] = __builtin_amdgcn_perm(b0, a0, 0x05010400u);
-        w[1] = __builtin_amdgcn_perm(b0, a0, 0x07030602u);
-        w[2] = __builtin_amdgcn_perm(b1, a1, 0x05010400u);
-        w[3] = __builtin_amdgcn_perm(b1, a1, 0x07030602u);
-      } else {
-        slow(u, w);
-      }
+    auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
+      const uint32_t i = 8 * u;
+      const uint64_t p0 = lds64(X, base + i), p1 = lds64(X, base + N + i);
+      const uint32_t a0 = (uint32_t)p0, a1 = (uint32_t)(p0 >> 32);
+      const uint32_t b0 = (uint32_t)p1, b1 = (uint32_t)(p1 >> 32);
+      w[0] = __builtin_amdgcn_perm(b0, a0, 0x05010400u);
+      w[1] = __builtin_amdgcn_perm(b0, a0, 0x07030602u);
+      w[2] = __builtin_amdgcn_perm(b1, a1, 0x05010400u);
+      w[3] = __builtin_amdgcn_perm(b1, a1, 0x07030602u);
+    };
+    drive2<16>(L, n, full / 16, final, gout, fast, [&](uint32_t u, uint32_t (&w)[4]) {
+      if (16 * u + 16 <= full) fast(u, w);
+      else slow(u, w);
     });
   } else {  // TS == 8: 32-B units = 4 elements
     const uint32_t full32 = (N * TS) & ~31u;
-    drive<32>(L, n, final, gout, [&](uint32_t u, uint32_t (&w)[8]) {
+    auto fast = [&](uint32_t u, uint32_t (&w)[8]) {
+      const uint32_t i = 4 * u;
+      uint32_t p[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) p[j] = lds32(X, base + j * N + i);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t q0 = p[4 * h], q1 = p[4 * h + 1], q2 = p[4 * h + 2], q3 = p[4 * h + 3];
+        const uint32_t a = __builtin_amdgcn_perm(q1, q0, 0x05010400u);
+        const uint32_t b = __builtin_amdgcn_perm(q3, q2, 0x05010400u);
+        const uint32_t c = __builtin_amdgcn_perm(q1, q0, 0x07030602u);
+        const uint32_t d = __builtin_amdgcn_perm(q3, q2, 0x07030602u);
+        w[0 + h] = __builtin_amdgcn_perm(b, a, 0x05040100u);  // element 0 low/high
+        w[2 + h] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // element 1
+        w[4 + h] = __builtin_amdgcn_perm(d, c, 0x05040100u);  // element 2
+        w[6 + h] = __builtin_amdgcn_perm(d, c, 0x07060302u);  // element 3
+      }
+    };
+    drive2<32>(L, n, full32 / 32, final, gout, fast, [&](uint32_t u, uint32_t (&w)[8]) {
       if (32 * u + 32 <= full32) {
-        const uint32_t i = 4 * u;
-        uint32_t p[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) p[j] = lds32(X, base + j * N + i);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const uint32_t q0 = p[4 * h], q1 = p[4 * h + 1], q2 = p[4 * h + 2], q3 = p[4 * h + 3];
-          const uint32_t a = __builtin_amdgcn_perm(q1, q0, 0x05010400u);
-          const uint32_t b = __builtin_amdgcn_perm(q3, q2, 0x05010400u);
-          const uint32_t c = __builtin_amdgcn_perm(q1, q0, 0x07030602u);
-          const uint32_t d = __builtin_amdgcn_perm(q3, q2, 0x07030602u);
-          w[0 + h] = __builtin_amdgcn_perm(b, a, 0x05040100u);  // element 0 low/high
-          w[2 + h] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // element 1
-          w[4 + h] = __builtin_amdgcn_perm(d, c, 0x05040100u);  // element 2
-          w[6 + h] = __builtin_amdgcn_perm(d, c, 0x07060302u);  // element 3
-        }
+        fast(u, w);
       } else {
         slow(2 * u, w);
         slow(2 * u + 1, w + 4);
@@ -516,8 +571,71 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     const uint32_t w = pow2 ? (o >> wsh) : (o / ws0);
     return w < nw ? w : nw - 1;
   };
-  if (W == 8) {
-    drive<16>(L, orig, final, gout, [&](uint32_t u, uint32_t (&wv)[4]) {
+  if ((W == 4 || W == 8) && ws0 % 16 == 0) {
+    // Every 16-B output unit lies in one window: one TAB read per unit, the
+    // unit's source bytes read as one aligned span, elements extracted in
+    // registers.  Compressed elements of a unit span at most 8 bytes.
+    constexpr uint32_t NE = 16 / W;
+    auto fn16 = [&](uint32_t u, uint32_t (&wv)[4]) {
+      const uint32_t o = 16 * u, w = win(o);
+      const uint4 e = L.TAB[w];
+      const uint32_t ob = o - w * ws0;
+      const bool raw = (e.y & 0x100u) != 0;
+      const uint32_t cb = (e.y & 0xffu) >> 3;
+      const uint32_t src = base + e.x + (raw ? ob : (ob / W) * cb);
+      const uint32_t a = src & ~3u, sh = src & 3u;
+      uint32_t d[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) d[k] = *(const uint32_t*)(X + a + 4 * k);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      if (raw) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) wv[k] = q[k];
+        return;
+      }
+      const uint64_t Q = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+      const uint64_t off = ((uint64_t)e.w << 32) | e.z;
+      const uint32_t bitsz = 8 * cb;
+#pragma unroll
+      for (uint32_t k = 0; k < NE; k++) {
+        uint64_t v = Q >> (bitsz * k);
+        v = bitsz >= 64 ? v : (v & ((1ull << bitsz) - 1));
+        if (SGN) v = (uint64_t)sext64(v, cb);
+        v += off;
+        if (W == 4) {
+          wv[k] = (uint32_t)v;
+        } else {
+          wv[2 * k] = (uint32_t)v;
+          wv[2 * k + 1] = (uint32_t)(v >> 32);
+        }
+      }
+    };
+    drive2<16>(L, orig, orig / 16, final, gout, fn16, [&](uint32_t u, uint32_t (&wv)[4]) {
+      // partial last unit: element-wise (the window may hold fewer bytes)
+#pragma unroll
+      for (uint32_t k = 0; k < NE; k++) {
+        const uint32_t o = 16 * u + W * k;
+        const uint32_t w = win(o);
+        const uint4 e = L.TAB[w];
+        const uint32_t ob = o - w * ws0;
+        uint64_t v = 0;
+        if (o < orig) {
+          if (e.y & 0x100u) v = ldsn(X, base + e.x + ob, W);
+          else v = bwr_elem<W, SGN>(X, base, e, ob / W);
+        }
+        if (W == 4) {
+          wv[k] = (uint32_t)v;
+        } else {
+          wv[2 * k] = (uint32_t)v;
+          wv[2 * k + 1] = (uint32_t)(v >> 32);
+        }
+      }
+    });
+  } else if (W == 8) {
+    auto fn = [&](uint32_t u, uint32_t (&wv)[4]) {
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t o = 16 * u + 8 * h;
@@ -530,9 +648,10 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         wv[2 * h] = (uint32_t)v;
         wv[2 * h + 1] = (uint32_t)(v >> 32);
       }
-    });
+    };
+    drive2<16>(L, orig, orig / 16, final, gout, fn, fn);
   } else if (W == 4) {
-    drive<16>(L, orig, final, gout, [&](uint32_t u, uint32_t (&wv)[4]) {
+    auto fn = [&](uint32_t u, uint32_t (&wv)[4]) {
       uint32_t w = win(16 * u);
       uint4 e = L.TAB[w];
 #pragma unroll
@@ -544,7 +663,8 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         if (e.y & 0x100u) wv[d] = lds32(X, base + e.x + ob);
         else wv[d] = (uint32_t)bwr_elem<W, SGN>(X, base, e, ob >> 2);
       }
-    });
+    };
+    drive2<16>(L, orig, orig / 16, final, gout, fn, fn);
   } else {  // W == 2: two elements per dword, windows may end mid-dword
     drive<16>(L, orig, final, gout, [&](uint32_t u, uint32_t (&wv)[4]) {
 #pragma unroll
