@@ -16,36 +16,57 @@ LIB = os.path.join(HERE, "libtiledb_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 
-SOURCES = ["tdbg_kernels.hip", "tdbg_fast.hip", "tdbg_host.cpp"]
+NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART_HOST)
+# (source, object name, extra flags)
+UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_host.cpp", "tdbg_host", [])] +
+         [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
+          for k in range(NPART)])
 HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h"]
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _deps(src: str):
+    d = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in HEADERS]
+    d.append(os.path.join(ROOT, "include", "tiledb_amd.h"))
+    return d
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "tiledb_amd.h"))
+    t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _stale() -> bool:
+    return _newer(LIB, [d for src, _, _ in UNITS for d in _deps(src)])
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    objs = []
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}",
               "-I", os.path.join(ROOT, "include")]
-    for src in SOURCES:
-        obj = os.path.join(objdir, src + ".o")
-        cmd = [HIPCC] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
-        if src.endswith(".cpp"):
-            cmd = [HIPCC, "-x", "hip"] + common + ["-c", os.path.join(CSRC, src), "-o", obj]
+    jobs, objs = [], []
+    for src, name, extra in UNITS:
+        obj = os.path.join(objdir, name + ".o")
+        objs.append(obj)
+        if not force and not _newer(obj, _deps(src)):
+            continue
+        cmd = [HIPCC] + (["-x", "hip"] if src.endswith(".cpp") else []) + common + extra + [
+            "-c", os.path.join(CSRC, src), "-o", obj]
+        jobs.append(cmd)
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
-        objs.append(obj)
+
+    nproc = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(nproc) as ex:
+        list(ex.map(run, jobs))
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
     if verbose:

@@ -37,8 +37,8 @@ struct tdbg_plan {
   tdbg_stage s[TDBG_MAX_FILTERS];
 };
 
-#define TDBG_E_FALLBACK 100
-#define TDBG_PROF_PHASES 8  // fused-kernel phase clocks per workgroup  // internal: fast path declined the tile
+#define TDBG_E_FALLBACK 100  // internal status: the fast path declined the tile
+#define TDBG_PROF_PHASES 8  // fused-kernel phase clocks per workgroup
 
 enum tdbg_fast_kind : uint32_t {
   TDBG_FAST_NONE = 0,
@@ -60,7 +60,13 @@ struct KParams {
   uint64_t slot_bytes;
   uint32_t slot_cap, md_cap, tab_cap;
   uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
-  uint32_t fixup;     // general kernel: only tiles whose status is TDBG_E_FALLBACK
+  uint32_t fixup;     // general kernel: only the tiles queued in fbq (TDBG_E_FALLBACK)
+  // Fallback queue of this launch: fbq[0] = count, fbq[1 + k] = tile index.
+  // The fused kernel appends the tiles it declines; the fixup launch walks
+  // the queue and clears fbq_next[0], the queue the context's next launch
+  // appends to (two queues alternate per launch on the context's stream).
+  uint32_t* fbq;
+  uint32_t* fbq_next;
   uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
   tdbg_plan plan;
 };

@@ -1536,7 +1536,10 @@ unfilter_fused_kernel(const KParams kp) {
     }
     if (!hooked) hook();
     __syncthreads();  // LDS reads of this tile done before the next commit
-    if (tid_() == 0 && kp.status) kp.status[t] = rc;
+    if (tid_() == 0) {
+      if (kp.status) kp.status[t] = rc;
+      if (rc == TDBG_E_FALLBACK && kp.fbq) kp.fbq[1 + atomicAdd(kp.fbq, 1u)] = (uint32_t)t;
+    }
     pc.mark(6);
   }
   pc.flush();
@@ -1590,6 +1593,15 @@ unfilter_fused_kernel(const KParams kp) {
   X(26, SC(K_BWR, 8, 0), 0, 0, 0)                                        \
   X(27, SC(K_BWR, 8, 1), 0, 0, 0)
 
+// The spec table is compiled as TDBG_NPART translation units (the build
+// passes -DTDBG_PART=k): part k instantiates the kernels whose id % NPART == k,
+// so the heavy kernel instantiations compile in parallel.
+#ifndef TDBG_PART
+#define TDBG_PART 0
+#define TDBG_NPART 1
+#endif
+
+#if TDBG_PART == 0
 static uint32_t stage_code(const tdbg_stage& s) {
   switch (s.kind) {
     case TDBG_K_PASS: return SC(TDBG_K_PASS, 0, 0);
@@ -1617,18 +1629,32 @@ extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus) {
   return (uint32_t)cus * 2;  // two ~80 KB workgroups per CU
 }
 
-extern "C" hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid,
-                                       hipStream_t stream) {
+#endif  // TDBG_PART == 0
+
+namespace {
+template <int ID, int A, int B, int C, int D>
+hipError_t launch_spec(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream) {
+  if constexpr (ID % TDBG_NPART == TDBG_PART) {
+    hipLaunchKernelGGL((tdbg::unfilter_fused_kernel<A, B, C, D>), dim3(grid), dim3(tdbg::FNT), 0, stream,
+                       *kp);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+}  // namespace
+
+#define TDBG_CAT2(a, b) a##b
+#define TDBG_CAT(a, b) TDBG_CAT2(a, b)
+extern "C" hipError_t TDBG_CAT(tdbg_launch_fast_part, TDBG_PART)(const tdbg::KParams* kp, uint32_t grid,
+                                                                 hipStream_t stream) {
   switch (kp->plan.fast) {
-#define LAUNCH(id, a, b, cc, d)                                                              \
-    case id:                                                                               \
-      hipLaunchKernelGGL((tdbg::unfilter_fused_kernel<a, b, cc, d>), dim3(grid), dim3(tdbg::FNT), \
-                         0, stream, *kp);                                                   \
-      break;
+#define LAUNCH(id, a, b, cc, d) \
+    case id:                    \
+      return launch_spec<id, a, b, cc, d>(kp, grid, stream);
     SPECS(LAUNCH)
 #undef LAUNCH
     default:
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }

@@ -25,8 +25,21 @@
 
 extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
                                           hipStream_t stream);
-extern "C" hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid,
-                                       hipStream_t stream);
+#define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
+#define TDBG_DECL_PART(k) \
+  extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
+TDBG_DECL_PART(0)
+TDBG_DECL_PART(1)
+TDBG_DECL_PART(2)
+TDBG_DECL_PART(3)
+TDBG_DECL_PART(4)
+TDBG_DECL_PART(5)
+static hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream) {
+  static hipError_t (*const parts[TDBG_NPART_HOST])(const tdbg::KParams*, uint32_t, hipStream_t) = {
+      tdbg_launch_fast_part0, tdbg_launch_fast_part1, tdbg_launch_fast_part2,
+      tdbg_launch_fast_part3, tdbg_launch_fast_part4, tdbg_launch_fast_part5};
+  return parts[kp->plan.fast % TDBG_NPART_HOST](kp, grid, stream);
+}
 extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan);
 extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus);
 
@@ -104,6 +117,9 @@ struct tdbg_context {
   uint64_t status_cap = 0;
   uint32_t* d_list = nullptr;
   uint64_t list_cap = 0;
+  // fused-kernel fallback queues (KParams::fbq), alternating per launch
+  uint32_t* d_fbq[2] = {nullptr, nullptr};
+  uint32_t fbq_parity = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   uint64_t tiles_unfiltered = 0, bytes_unfiltered = 0;
@@ -148,6 +164,12 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   if (c->d_need) HIP_OK(hipFree(c->d_need));
   HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
   HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
+  for (auto*& q : c->d_fbq) {
+    if (q) HIP_OK(hipFree(q));
+    q = nullptr;
+    HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
+    HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
+  }
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -386,6 +408,8 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->d_need) (void)hipFree(c->d_need);
   if (c->d_list) (void)hipFree(c->d_list);
+  for (auto* q : c->d_fbq)
+    if (q) (void)hipFree(q);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -457,15 +481,21 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       kp.prof = c->d_prof;
     }
   }
+  if (fast && d_status && !kp.dbg_stop) {
+    kp.fbq = c->d_fbq[c->fbq_parity];
+    kp.fbq_next = c->d_fbq[c->fbq_parity ^ 1];
+    c->fbq_parity ^= 1;
+  }
   HIP_OK(hipEventRecord(c->ev0, stream));
   hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
   if (fast && d_status && !kp.dbg_stop) {
-    // tiles the fused kernel declined (status TDBG_E_FALLBACK) are redone by
-    // the general interpreter, same stream, no host round trip
+    // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
+    // are redone by the general interpreter, same stream, no host round trip;
+    // with an empty queue every workgroup exits after one load
     tdbg::KParams g = kp;
     g.fixup = 1;
-    e = tdbg_launch_general(&g, ggrid, stream);
+    e = tdbg_launch_general(&g, std::min<uint32_t>(ggrid, (uint32_t)c->cus), stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
   }
   HIP_OK(hipEventRecord(c->ev1, stream));

@@ -36,9 +36,15 @@ unfilter_general_kernel(const KParams kp) {
   sl.md[0] = base + 2ull * kp.slot_cap;
   sl.md[1] = sl.md[0] + kp.md_cap;
   sl.tab = sl.md[1] + kp.md_cap;
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
-    const uint64_t t = kp.tile_list ? kp.tile_list[j] : j;
-    if (kp.fixup && kp.status[t] != TDBG_E_FALLBACK) continue;  // uniform per workgroup
+  uint64_t n = kp.ntiles;
+  const uint32_t* list = kp.tile_list;
+  if (kp.fixup) {  // only the tiles the fused kernel queued (usually none)
+    n = kp.fbq[0];
+    list = kp.fbq + 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) kp.fbq_next[0] = 0;
+  }
+  for (uint64_t j = blockIdx.x; j < n; j += gridDim.x) {
+    const uint64_t t = list ? list[j] : j;
     uint64_t need = 0;
     const int rc = g_tile<GEN_NT>(kp, kp.in[t], kp.in_size[t], kp.out[t], kp.out_size[t], sl, sh, &need);
     __syncthreads();

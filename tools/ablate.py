@@ -1,5 +1,5 @@
 """Timing-only ablation of the fused kernel (TDBG_DEBUG_STOP = stop after N stages).
-Run on the GPU box: python tools_ablate.py  -> prints kernel ms per variant."""
+Run on the GPU box (repo root): python tools/ablate.py  -> prints kernel ms per variant."""
 import os, subprocess, sys, json
 res = {}
 for stop in ["1", "2", "3", "0"]:

@@ -1,0 +1,14 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench line.  Each GPU step is time-limited
+# and steps are chained so a failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/check_${1:-r01}
+mkdir -p $OUT
+cd $R
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 11; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 12; }
+cat $OUT/smoke.log
+timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 13; }
+cat $OUT/bench.log

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profile bench.py on the GPU box: kernel-trace/stats pass + separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE) -- never combined with sys/runtime traces.
-# usage: bash tools_profile.sh <tag> [bench args...]
+# usage: bash tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
