@@ -172,7 +172,7 @@ __device__ __forceinline__ bool load_to_lds(uint8_t* X, uint32_t cap, const uint
 __device__ __forceinline__ void store_unit(uint8_t* gout, uint32_t n, uint32_t off, uint4 v) {
   if (off + 16 <= n && (((uintptr_t)(gout + off)) & 15) == 0) {
     v4u x = {v.x, v.y, v.z, v.w};
-    *(g_u4*)(gout + off) = x;
+    __builtin_nontemporal_store(x, (g_u4*)(gout + off));
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -224,7 +224,7 @@ __device__ __forceinline__ void drive2(FastLds& L, uint32_t n, uint32_t nfast, b
 #pragma unroll
             for (int q = 0; q < UD / 4; q++) {
               v4u x = {w[r][4 * q], w[r][4 * q + 1], w[r][4 * q + 2], w[r][4 * q + 3]};
-              *(g_u4*)(gout + u * UB + 16 * q) = x;
+              __builtin_nontemporal_store(x, (g_u4*)(gout + u * UB + 16 * q));
             }
           }
         }

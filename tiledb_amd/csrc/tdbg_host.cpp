@@ -25,6 +25,8 @@
 
 extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
                                           hipStream_t stream);
+extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
+                                        hipStream_t stream);
 #define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
 #define TDBG_DECL_PART(k) \
   extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
@@ -495,7 +497,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     // with an empty queue every workgroup exits after one load
     tdbg::KParams g = kp;
     g.fixup = 1;
-    e = tdbg_launch_general(&g, std::min<uint32_t>(ggrid, (uint32_t)c->cus), stream);
+    e = tdbg_launch_fixup(&g, std::min<uint32_t>(ggrid, (uint32_t)c->cus), stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
   }
   HIP_OK(hipEventRecord(c->ev1, stream));

@@ -23,8 +23,7 @@
 
 namespace tdbg {
 
-__global__ void __launch_bounds__(GEN_NT)
-unfilter_general_kernel(const KParams kp) {
+__device__ __attribute__((noinline)) void general_body(const KParams& kp) {
   __shared__ Shared<GEN_NT> sh;
   Slot sl;
   uint8_t* base = kp.scratch + (uint64_t)blockIdx.x * kp.slot_bytes;
@@ -38,10 +37,9 @@ unfilter_general_kernel(const KParams kp) {
   sl.tab = sl.md[1] + kp.md_cap;
   uint64_t n = kp.ntiles;
   const uint32_t* list = kp.tile_list;
-  if (kp.fixup) {  // only the tiles the fused kernel queued (usually none)
+  if (kp.fixup) {  // only the tiles the fused kernel queued
     n = kp.fbq[0];
     list = kp.fbq + 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) kp.fbq_next[0] = 0;
   }
   for (uint64_t j = blockIdx.x; j < n; j += gridDim.x) {
     const uint64_t t = list ? list[j] : j;
@@ -55,6 +53,23 @@ unfilter_general_kernel(const KParams kp) {
   }
 }
 
+__global__ void __launch_bounds__(GEN_NT)
+unfilter_general_kernel(const KParams kp) {
+  general_body(kp);
+}
+
+// Fixup launch after the fused kernel: the general interpreter over the
+// tiles the fused kernel queued.  The queue is almost always empty, so the
+// entry only reads its count (the interpreter's prologue sits behind the call).
+__global__ void __launch_bounds__(GEN_NT)
+unfilter_fixup_kernel(const KParams kp) {
+  const uint32_t queued = kp.fbq[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) kp.fbq_next[0] = 0;
+  if (queued == 0) return;
+  const KParams local = kp;  // copied only past the early exit
+  general_body(local);
+}
+
 }  // namespace tdbg
 
 // ---------------------------------------------------------------------------
@@ -63,5 +78,11 @@ unfilter_general_kernel(const KParams kp) {
 extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
                                           hipStream_t stream) {
   hipLaunchKernelGGL(tdbg::unfilter_general_kernel, dim3(grid), dim3(GEN_NT), 0, stream, *kp);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
+                                        hipStream_t stream) {
+  hipLaunchKernelGGL(tdbg::unfilter_fixup_kernel, dim3(grid), dim3(GEN_NT), 0, stream, *kp);
   return hipGetLastError();
 }
