@@ -209,6 +209,15 @@ int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
  * hipEvents recorded around the kernel on its stream (ms). */
 int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
 
+/* Per-launch device timing for benchmarks: arm event recording for the next
+ * n tdbg_unfilter_tiles_* launches on ctx, then read them back (waits for the
+ * last armed launch): kernel_ms[i] = the fused (or general) unfilter kernel of
+ * launch i alone, total_ms[i] = that kernel plus its fallback fixup launch.
+ * Either output may be NULL; reading disarms. */
+int tdbg_context_time_launches(tdbg_context* ctx, uint32_t n);
+int tdbg_context_launch_times(tdbg_context* ctx, float* kernel_ms, float* total_ms,
+                              uint32_t cap, uint32_t* count);
+
 /* Diagnostics (no reference counterpart): with TDBG_PROF=1 in the
  * environment, the fused kernel accumulates shader-clock cycles per phase
  * (0 tile wait, 1 headers, 2-4 intermediate stages, 5 final stage, 6 loop

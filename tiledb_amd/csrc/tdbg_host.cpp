@@ -124,6 +124,10 @@ struct tdbg_context {
   uint32_t fbq_parity = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  // armed per-launch timing (tdbg_context_time_launches): event triples
+  // {before the fused/general kernel, after it, after the fixup launch}
+  std::vector<hipEvent_t> tev;
+  uint32_t tcap = 0, tcount = 0;
   uint64_t tiles_unfiltered = 0, bytes_unfiltered = 0;
   // host E2E staging
   struct Stage {
@@ -426,6 +430,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->d_prof) (void)hipFree(c->d_prof);
+  for (auto e : c->tev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -488,9 +493,12 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kp.fbq_next = c->d_fbq[c->fbq_parity ^ 1];
     c->fbq_parity ^= 1;
   }
+  hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   HIP_OK(hipEventRecord(c->ev0, stream));
+  if (te) HIP_OK(hipEventRecord(te[0], stream));
   hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  if (te) HIP_OK(hipEventRecord(te[1], stream));
   if (fast && d_status && !kp.dbg_stop) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
@@ -501,6 +509,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
   }
   HIP_OK(hipEventRecord(c->ev1, stream));
+  if (te) HIP_OK(hipEventRecord(te[2], stream));
   c->timed = true;
   return TDBG_OK;
 }
@@ -601,6 +610,34 @@ int tdbg_context_stats(const tdbg_context* c, uint64_t* tiles, uint64_t* bytes) 
   if (!c) return fail(TDBG_E_ARG, "null context");
   if (tiles) *tiles = c->tiles_unfiltered;
   if (bytes) *bytes = c->bytes_unfiltered;
+  return TDBG_OK;
+}
+
+int tdbg_context_time_launches(tdbg_context* c, uint32_t n) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  HIP_OK(hipSetDevice(c->device));
+  while (c->tev.size() < 3ull * n) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    c->tev.push_back(e);
+  }
+  c->tcap = n;
+  c->tcount = 0;
+  return TDBG_OK;
+}
+
+int tdbg_context_launch_times(tdbg_context* c, float* kernel_ms, float* total_ms, uint32_t cap,
+                              uint32_t* count) {
+  if (!c || !count) return fail(TDBG_E_ARG, "null argument");
+  const uint32_t n = std::min(c->tcount, cap);
+  for (uint32_t i = 0; i < n; i++) {
+    HIP_OK(hipEventSynchronize(c->tev[3 * i + 2]));
+    if (kernel_ms) HIP_OK(hipEventElapsedTime(&kernel_ms[i], c->tev[3 * i], c->tev[3 * i + 1]));
+    if (total_ms) HIP_OK(hipEventElapsedTime(&total_ms[i], c->tev[3 * i], c->tev[3 * i + 2]));
+  }
+  *count = n;
+  c->tcap = 0;  // disarm
+  c->tcount = 0;
   return TDBG_OK;
 }
 

@@ -186,6 +186,20 @@ class Context:
         _check(lib.tdbg_context_last_kernel_ms(self.h, ctypes.byref(ms)), "last_kernel_ms")
         return float(ms.value)
 
+    def time_launches(self, n: int) -> None:
+        """Arm per-launch HIP-event timing for the next n launches on this context."""
+        _check(lib.tdbg_context_time_launches(self.h, n), "tdbg_context_time_launches")
+
+    def launch_times(self, cap: int = 4096):
+        """(kernel_ms, total_ms) per armed launch: the unfilter kernel alone, and
+        with its fallback fixup launch (waits for the last armed launch)."""
+        k = np.zeros(cap, dtype=np.float32)
+        t = np.zeros(cap, dtype=np.float32)
+        n = ctypes.c_uint32()
+        _check(lib.tdbg_context_launch_times(self.h, k.ctypes.data, t.ctypes.data, cap,
+                                             ctypes.byref(n)), "tdbg_context_launch_times")
+        return k[: n.value].copy(), t[: n.value].copy()
+
     def phase_clocks(self, nphases: int = 8) -> np.ndarray:
         """Diagnostics: fused-kernel cycles per phase of the last launch (TDBG_PROF=1)."""
         out = np.zeros(nphases, dtype=np.uint64)
