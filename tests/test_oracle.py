@@ -332,3 +332,20 @@ def test_mt_batch_equals_single(oracle_mod):
     assert rc == 0 and not st.any()
     for i, v in enumerate(vals):
         assert np.array_equal(out[i * 65536:(i + 1) * 65536], v.view(np.uint8))
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c2i", "c3a", "c3b", "c4", "c5"])
+def test_numpy_config_encoders_match_oracle(oracle_mod, name):
+    """workloads.py's forward restatements (the bench's inputs) equal the
+    oracle's forward pass byte for byte, and unfilter back to the values."""
+    import workloads as W
+    ser, dt, cs, values, tile = W.config(name)
+    op = oracle_mod.OraclePipeline(ser, 23, int(dt), cs)
+    rng = np.random.default_rng(7)
+    for variant in ("ramp", "rand"):
+        for k in range(3):
+            v = values(variant, k, rng)
+            f = tile(v)
+            assert f == op.filter_tile(v), f"{name} {variant} tile {k}"
+            rc, out = op.unfilter_tile(f, v.nbytes)
+            assert rc == 0 and np.array_equal(out, v.view(np.uint8))

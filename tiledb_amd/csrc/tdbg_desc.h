@@ -34,6 +34,7 @@ struct tdbg_stage {
 struct tdbg_plan {
   uint32_t nstages;
   uint32_t fast;  // fused fast-path selector (tdbg_fast_kind), 0 = none
+  uint32_t view;  // streaming view-kernel selector (tdbg_view.hip), 0 = none
   tdbg_stage s[TDBG_MAX_FILTERS];
 };
 
@@ -67,6 +68,11 @@ struct KParams {
   // appends to (two queues alternate per launch on the context's stream).
   uint32_t* fbq;
   uint32_t* fbq_next;
+  // LDS queue (same layout as fbq): the view kernel appends the tiles it
+  // cannot stream; the fused kernel, when ldsq is set, walks that queue
+  // instead of all ntiles.  ldsq_next[0] is cleared by the fixup launch.
+  uint32_t* ldsq;
+  uint32_t* ldsq_next;
   uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
   tdbg_plan plan;
 };

@@ -1403,11 +1403,11 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ TileDesc desc_load(const KParams& kp, uint64_t j) {
+__device__ __forceinline__ TileDesc desc_load(const KParams& kp, const uint32_t* tl, uint64_t j) {
   uint32_t z = 0;
   asm volatile("" : "+v"(z));
   TileDesc d;
-  d.t = kp.tile_list ? kp.tile_list[j + z] : j + z;
+  d.t = tl ? tl[j + z] : j + z;
   d.fs = kp.in_size[d.t + z];
   d.os = kp.out_size[d.t + z];
   d.in = kp.in[d.t + z];
@@ -1437,12 +1437,19 @@ unfilter_fused_kernel(const KParams kp) {
   pf.cnt = 0;
   pf.base = 0;
   constexpr bool PF = pf_enabled(S0, S1, S2, S3);
+  // tiles: all ntiles, a host-given list (retry), or the view kernel's queue
+  uint64_t ntl = kp.ntiles;
+  const uint32_t* tl = kp.tile_list;
+  if (kp.ldsq) {
+    ntl = __builtin_amdgcn_readfirstlane(kp.ldsq[0]);
+    tl = kp.ldsq + 1;
+  }
   TileDesc dn{};
-  if (blockIdx.x < kp.ntiles) {
-    dn = desc_uniform(desc_load(kp, blockIdx.x));
+  if (blockIdx.x < ntl) {
+    dn = desc_uniform(desc_load(kp, tl, blockIdx.x));
     if (PF) pf_issue(pf, dn.in, dn.fs);
   }
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += G) {
+  for (uint64_t j = blockIdx.x; j < ntl; j += G) {
     const TileDesc d = dn;
     const uint64_t t = d.t;
     const uint8_t* in = d.in;
@@ -1451,11 +1458,11 @@ unfilter_fused_kernel(const KParams kp) {
     const uint64_t os = d.os;
     const uint64_t jn = j + G;
     TileDesc dl{};
-    if (jn < kp.ntiles) dl = desc_load(kp, jn);  // consumed by the hook
+    if (jn < ntl) dl = desc_load(kp, tl, jn);  // consumed by the hook
     bool hooked = false;
     auto hook = [&]() {
       hooked = true;
-      if (jn < kp.ntiles) {
+      if (jn < ntl) {
         dn = desc_uniform(dl);
         if (PF) pf_issue(pf, dn.in, dn.fs);
       } else {

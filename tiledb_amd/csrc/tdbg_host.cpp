@@ -27,6 +27,8 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
                                           hipStream_t stream);
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
+extern "C" hipError_t tdbg_launch_view(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
+extern "C" uint32_t tdbg_view_select(const tdbg_plan* plan);
 #define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
 #define TDBG_DECL_PART(k) \
   extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
@@ -121,6 +123,7 @@ struct tdbg_context {
   uint64_t list_cap = 0;
   // fused-kernel fallback queues (KParams::fbq), alternating per launch
   uint32_t* d_fbq[2] = {nullptr, nullptr};
+  uint32_t* d_ldsq[2] = {nullptr, nullptr};  // view kernel -> fused kernel queues (KParams::ldsq)
   uint32_t fbq_parity = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -170,12 +173,14 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   if (c->d_need) HIP_OK(hipFree(c->d_need));
   HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
   HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
-  for (auto*& q : c->d_fbq) {
-    if (q) HIP_OK(hipFree(q));
-    q = nullptr;
-    HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
-    HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
-  }
+  for (uint32_t** qs : {c->d_fbq, c->d_ldsq})
+    for (int k = 0; k < 2; k++) {
+      uint32_t*& q = qs[k];
+      if (q) HIP_OK(hipFree(q));
+      q = nullptr;
+      HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
+      HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
+    }
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -265,6 +270,7 @@ void build_plan(tdbg_pipeline* p) {
     }
   }
   P.fast = p->supported ? tdbg_fast_select(&P) : 0;
+  P.view = P.fast ? tdbg_view_select(&P) : 0;
 }
 
 }  // namespace
@@ -416,6 +422,8 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_list) (void)hipFree(c->d_list);
   for (auto* q : c->d_fbq)
     if (q) (void)hipFree(q);
+  for (auto* q : c->d_ldsq)
+    if (q) (void)hipFree(q);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -488,18 +496,38 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       kp.prof = c->d_prof;
     }
   }
-  if (fast && d_status && !kp.dbg_stop) {
+  const bool queued = fast && d_status && !kp.dbg_stop;
+  // streaming view kernel first (tdbg_view.hip) when the pipeline has the
+  // byteshuffle[-DD][-BWR] shape; it queues non-view tiles for the fused kernel
+  // (opt-in while the streaming path is being validated on hardware)
+  static const bool use_view = getenv("TDBG_VIEW") != nullptr && getenv("TDBG_NO_VIEW") == nullptr;
+  const bool view = queued && !d_list && p->plan.view != 0 && use_view;
+  if (queued) {
     kp.fbq = c->d_fbq[c->fbq_parity];
     kp.fbq_next = c->d_fbq[c->fbq_parity ^ 1];
+    kp.ldsq_next = c->d_ldsq[c->fbq_parity ^ 1];
     c->fbq_parity ^= 1;
   }
-  hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
+  hipEvent_t* te = c->tcount < c->tcap ? &c->tev[4 * c->tcount++] : nullptr;
   HIP_OK(hipEventRecord(c->ev0, stream));
   if (te) HIP_OK(hipEventRecord(te[0], stream));
-  hipError_t e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
-  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  hipError_t e;
+  if (view) {
+    kp.ldsq = c->d_ldsq[c->fbq_parity ^ 1];  // this launch's queue (parity flipped above)
+    e = tdbg_launch_view(&kp, (uint32_t)c->cus * 8, stream);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("view launch: ") + hipGetErrorString(e));
+  }
   if (te) HIP_OK(hipEventRecord(te[1], stream));
-  if (fast && d_status && !kp.dbg_stop) {
+  static const bool view_only = getenv("TDBG_DEBUG_VIEW_ONLY") != nullptr;  // diagnostics
+  if (view && view_only) {
+    HIP_OK(hipEventRecord(c->ev1, stream));
+    c->timed = true;
+    return TDBG_OK;
+  }
+  e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  if (te) HIP_OK(hipEventRecord(te[2], stream));
+  if (queued) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
     // with an empty queue every workgroup exits after one load
@@ -509,7 +537,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
   }
   HIP_OK(hipEventRecord(c->ev1, stream));
-  if (te) HIP_OK(hipEventRecord(te[2], stream));
+  if (te) HIP_OK(hipEventRecord(te[3], stream));
   c->timed = true;
   return TDBG_OK;
 }
@@ -616,7 +644,7 @@ int tdbg_context_stats(const tdbg_context* c, uint64_t* tiles, uint64_t* bytes) 
 int tdbg_context_time_launches(tdbg_context* c, uint32_t n) {
   if (!c) return fail(TDBG_E_ARG, "null context");
   HIP_OK(hipSetDevice(c->device));
-  while (c->tev.size() < 3ull * n) {
+  while (c->tev.size() < 4ull * n) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     c->tev.push_back(e);
@@ -626,14 +654,16 @@ int tdbg_context_time_launches(tdbg_context* c, uint32_t n) {
   return TDBG_OK;
 }
 
-int tdbg_context_launch_times(tdbg_context* c, float* kernel_ms, float* total_ms, uint32_t cap,
-                              uint32_t* count) {
+int tdbg_context_launch_times(tdbg_context* c, float* view_ms, float* kernel_ms, float* total_ms,
+                              uint32_t cap, uint32_t* count) {
   if (!c || !count) return fail(TDBG_E_ARG, "null argument");
   const uint32_t n = std::min(c->tcount, cap);
   for (uint32_t i = 0; i < n; i++) {
-    HIP_OK(hipEventSynchronize(c->tev[3 * i + 2]));
-    if (kernel_ms) HIP_OK(hipEventElapsedTime(&kernel_ms[i], c->tev[3 * i], c->tev[3 * i + 1]));
-    if (total_ms) HIP_OK(hipEventElapsedTime(&total_ms[i], c->tev[3 * i], c->tev[3 * i + 2]));
+    hipEvent_t* e = &c->tev[4 * i];
+    HIP_OK(hipEventSynchronize(e[3]));
+    if (view_ms) HIP_OK(hipEventElapsedTime(&view_ms[i], e[0], e[1]));
+    if (kernel_ms) HIP_OK(hipEventElapsedTime(&kernel_ms[i], e[1], e[2]));
+    if (total_ms) HIP_OK(hipEventElapsedTime(&total_ms[i], e[0], e[3]));
   }
   *count = n;
   c->tcap = 0;  // disarm

@@ -1,8 +1,9 @@
 """Synthetic BASELINE workloads for bench.py (numpy, independent of oracle/).
 
-Writes on-disk filtered tiles for the C5 pipeline
-[BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)] on INT32,
-restating the forward direction of
+Writes on-disk filtered tiles for every BASELINE config: C1
+[BYTESHUFFLE], C2/C2i [BITSHUFFLE, BWR], C3a [DD], C3b [RLE], C4 [PD, BWR] and
+the headline C5 [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)] on
+INT32, restating the forward direction of
   ByteshuffleFilter::run_forward      byteshuffle_filter.cc:60-89
   CompressionFilter::run_forward      compression_filter.cc:240-301
   DoubleDelta::compress<int>          dd_compressor.cc:211-312
@@ -97,6 +98,257 @@ def c5_filter_tile(values: np.ndarray) -> bytes:
     bwr_md, bwr_data = _bwr_int32(c0 + c1, 256)
     md = bwr_md + dd_md
     return struct.pack("<QIII", 1, nbytes, len(bwr_data), len(md)) + md + bwr_data
+
+
+# ---------------------------------------------------------------------------
+# generic forward restatements (numpy) for the other BASELINE configs
+# ---------------------------------------------------------------------------
+_UT = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
+_ST = {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}
+
+
+def tile_image(orig: int, md: bytes, data: bytes) -> bytes:
+    """One-chunk tile: [u64 1][u32 orig][u32 filtered][u32 md_len][md][data]
+    (filter_pipeline.cc:332-363, format_spec/tile.md)."""
+    return struct.pack("<QIII", 1, orig, len(data), len(md)) + md + data
+
+
+def byteshuffle_fwd(data: bytes, ts: int) -> bytes:
+    """blosc2 generic shuffle (byteshuffle_filter.cc:97): byte planes, tail kept."""
+    b = np.frombuffer(data, dtype=np.uint8)
+    n = b.size // ts
+    body = b[: n * ts].reshape(n, ts).T.reshape(-1)
+    return body.tobytes() + b[n * ts:].tobytes()
+
+
+def bitshuffle_fwd(data: bytes, ts: int) -> Tuple[bytes, bytes]:
+    """BitshuffleFilter::run_forward (bitshuffle_filter.cc:60-126) -> (md, data):
+    parts [size - size%8][size%8]; a part is transformed in 8192-B blocks when
+    size % 8 == 0 and size % ts == 0 (bit planes of the first n - n%8 elements)."""
+    b = np.frombuffer(data, dtype=np.uint8)
+    parts = [b[: b.size - b.size % 8]] + ([b[b.size - b.size % 8:]] if b.size % 8 else [])
+    out = []
+    for part in parts:
+        if part.size % 8 or part.size % ts:
+            out.append(part.tobytes())
+            continue
+        for o in range(0, part.size, 8192):
+            blk = part[o:o + 8192]
+            ne = blk.size // ts
+            n8 = ne - ne % 8
+            x = blk[: n8 * ts].reshape(n8, ts)
+            bits = np.unpackbits(x, axis=1, bitorder="little")          # (n8, 8ts): col 8b+k
+            planes = np.packbits(bits.T, axis=1, bitorder="little")      # (8ts, n8/8)
+            out.append(planes.tobytes() + blk[n8 * ts:].tobytes())
+    md = struct.pack("<I", len(parts)) + b"".join(struct.pack("<I", p.size) for p in parts)
+    return md, b"".join(out)
+
+
+def bwr_fwd(data: bytes, window: int, w: int, signed: bool) -> Tuple[bytes, bytes]:
+    """BitWidthReductionFilter::run_forward<T> (bit_width_reduction_filter.cc:167-280,
+    406-447); the offset of an overflowing window is written as 0 (the reference
+    leaves it uninitialized)."""
+    L = len(data)
+    ws = min(L, window) // w * w
+    nwin = L // ws + (1 if L % ws else 0)
+    md = [struct.pack("<II", L, nwin)]
+    out = []
+    buf = np.frombuffer(data, dtype=np.uint8)
+    lim = (1 << (8 * w - 1)) - 1 if signed else (1 << (8 * w)) - 1
+    for k in range(nwin):
+        nb = min(ws, L - k * ws)
+        ne = nb // w
+        seg = buf[k * ws: k * ws + nb]
+        bits, minv = 8 * w, 0
+        if ne:
+            vals = seg[: ne * w].view(("<i" if signed else "<u") + str(w))
+            mn, mx = int(vals.min()), int(vals.max())
+            rng = mx - mn
+            if rng <= lim and rng + 1 <= lim:
+                ro = rng + 1
+                if signed:
+                    bits = 8 if ro <= 127 else 16 if ro <= 32767 else 32 if ro <= 2**31 - 1 else 64
+                else:
+                    nbits = ro.bit_length()
+                    bits = 8 if nbits <= 8 else 16 if nbits <= 16 else 32 if nbits <= 32 else 64
+                minv = mn
+        fmt = "<" + ({1: "b", 2: "h", 4: "i", 8: "q"} if signed else {1: "B", 2: "H", 4: "I", 8: "Q"})[w]
+        md.append(struct.pack(fmt, minv) + struct.pack("<BI", bits, nb))
+        if bits >= 8 * w or nb % w:
+            out.append(seg.tobytes())
+        else:
+            rel = (vals.astype(np.int64 if signed else np.uint64) -
+                   np.array(minv, dtype=np.int64 if signed else np.uint64))
+            out.append(rel.astype(_UT[bits // 8]).tobytes())
+    return b"".join(md), b"".join(out)
+
+
+def dd_fwd(v: np.ndarray, w: int) -> bytes:
+    """DoubleDelta::compress<T> (dd_compressor.cc:211-312); v holds the T values."""
+    n = v.size
+    x = v.astype(np.int64)
+    if n <= 2:
+        b = 0
+    else:
+        d = np.diff(x)
+        dd = np.diff(d)
+        m = max(int(np.abs(d[0])), int(np.abs(dd).max()) if dd.size else 0)
+        b = max(1, int(m).bit_length())
+    hdr = struct.pack("<BQ", b, n)
+    raw = v.astype(("<u" if v.dtype.kind == "u" else "<i") + str(w)).tobytes()
+    if b >= 8 * w - 1:
+        return hdr + raw
+    out = hdr + raw[: w * min(n, 2)]
+    if n <= 2:
+        return out
+    d = np.diff(x)
+    dd = np.diff(d)
+    sign = (dd < 0).astype(np.uint8)
+    mag = np.abs(dd).astype(np.uint64)
+    shifts = np.arange(b - 1, -1, -1, dtype=np.uint64)
+    bits = ((mag[:, None] >> shifts[None, :]) & np.uint64(1)).astype(np.uint8)
+    codes = np.concatenate([sign[:, None], bits], axis=1).reshape(-1)
+    pad = (-codes.size) % 64
+    codes = np.concatenate([codes, np.zeros(pad, dtype=np.uint8)])
+    be = np.packbits(codes.reshape(-1, 64), axis=1, bitorder="big")  # MSB-first per word
+    return out + be.view(">u8").reshape(-1).astype("<u8").tobytes()
+
+
+def rle_fwd(data: bytes, cs: int) -> bytes:
+    """RLE::compress (rle_compressor.cc:51-101): [value][len_hi][len_lo], runs <= 65535."""
+    v = np.frombuffer(data, dtype=np.uint8).reshape(-1, cs)
+    keys = v.view(np.dtype((np.void, cs))).reshape(-1)
+    starts = np.concatenate([[0], np.nonzero(keys[1:] != keys[:-1])[0] + 1, [keys.size]])
+    out = []
+    for a, e in zip(starts[:-1], starts[1:]):
+        n = int(e - a)
+        while n > 0:
+            k = min(n, 65535)
+            out.append(v[a].tobytes() + bytes([k >> 8, k & 255]))
+            n -= k
+    return b"".join(out)
+
+
+def pd_fwd(data: bytes, window: int, w: int) -> Tuple[bytes, bytes]:
+    """PositiveDeltaFilter::run_forward<T> (positive_delta_filter.cc:140-245);
+    the input is nondecreasing (offsets), so no window errors."""
+    L = len(data)
+    ws = min(L, window) // w * w
+    nwin = L // ws + (1 if L % ws else 0)
+    buf = np.frombuffer(data, dtype=np.uint8)
+    md, out = [struct.pack("<I", nwin)], []
+    for k in range(nwin):
+        nb = min(ws, L - k * ws)
+        seg = buf[k * ws: k * ws + nb]
+        first = seg[:w].tobytes() if seg.size >= w else seg.tobytes().ljust(w, b"\0")
+        md.append(first + struct.pack("<I", nb))
+        if nb % w:
+            out.append(seg.tobytes())
+        else:
+            vals = seg.view("<u" + str(w)).astype(np.uint64)
+            d = np.diff(vals, prepend=vals[:1])
+            out.append(d.astype(_UT[w]).tobytes())
+    return b"".join(md), b"".join(out)
+
+
+def comp_frame(md_parts, data_parts) -> bytes:
+    """CompressionFilter metadata (compression_filter.cc:269-300)."""
+    h = struct.pack("<II", len(md_parts), len(data_parts))
+    return h + b"".join(struct.pack("<II", u, c) for u, c in list(md_parts) + list(data_parts))
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs C1-C4 (SURVEY.md 8(d)); values per config, tiles on disk
+# ---------------------------------------------------------------------------
+def c1_values(variant: str, k: int, rng: np.random.Generator) -> np.ndarray:
+    """2D int32 2048x2048, 128x128 tiles: a[r][c] = r*2048 + c + 1 (ramp)."""
+    if variant == "rand":
+        return rng.integers(-2**31, 2**31, 16384, dtype=np.int64).astype(np.int32)
+    tr, tc = divmod(k % 256, 16)
+    r = np.arange(128)[:, None] + 128 * tr
+    c = np.arange(128)[None, :] + 128 * tc
+    return (r * 2048 + c + 1).astype(np.int32).reshape(-1)
+
+
+def c1_tile(v: np.ndarray) -> bytes:
+    raw = v.astype("<i4").tobytes()
+    return tile_image(len(raw), struct.pack("<II", 1, len(raw)), byteshuffle_fwd(raw, 4))
+
+
+def c2_values(k: int, rng: np.random.Generator) -> np.ndarray:
+    g = np.arange(16384, dtype=np.float64) + 16384 * k
+    return (1000.0 * np.sin(1e-3 * g) + rng.normal(0, 0.01, 16384)).astype(np.float32)
+
+
+def c2_tile(v: np.ndarray, int_typed: bool) -> bytes:
+    raw = v.tobytes()
+    bmd, bdata = bitshuffle_fwd(raw, 4)
+    if not int_typed:  # BWR on FLOAT32 is a pass-through (bwr.cc:166-176)
+        return tile_image(len(raw), bmd, bdata)
+    wmd, wdata = bwr_fwd(bdata, 256, 4, True)
+    return tile_image(len(raw), wmd + bmd, wdata)
+
+
+def c3_values(k: int, rng: np.random.Generator) -> np.ndarray:
+    """Sorted uint64 coords: runs of 64 equal values, gaps U{1..16}."""
+    steps = np.zeros(8192, dtype=np.uint64)
+    steps[64::64] = rng.integers(1, 17, 8192 // 64 - 1).astype(np.uint64)
+    return np.uint64(1000 * k) + np.cumsum(steps, dtype=np.uint64)
+
+
+def c3a_tile(v: np.ndarray) -> bytes:
+    c = dd_fwd(v, 8)
+    return tile_image(v.nbytes, comp_frame([], [(v.nbytes, len(c))]), c)
+
+
+def c3b_tile(v: np.ndarray) -> bytes:
+    c = rle_fwd(v.astype("<u8").tobytes(), 8)
+    return tile_image(v.nbytes, comp_frame([], [(v.nbytes, len(c))]), c)
+
+
+def c4_values(k: int, rng: np.random.Generator) -> np.ndarray:
+    lens = rng.integers(0, 33, 8192).astype(np.uint64)
+    offs = np.zeros(8192, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return offs
+
+
+def c4_tile(v: np.ndarray) -> bytes:
+    raw = v.astype("<u8").tobytes()
+    pmd, pdata = pd_fwd(raw, 1024, 8)
+    wmd, wdata = bwr_fwd(pdata, 256, 8, False)
+    return tile_image(len(raw), wmd + pmd, wdata)
+
+
+def config(name: str):
+    """(serialized pipeline, on-disk datatype, cell size, values(variant, k, rng), tile(values))."""
+    from tiledb_amd.filter_pipeline import (BitshuffleFilter, BitWidthReductionFilter,
+                                            ByteshuffleFilter, CompressionFilter, Compressor,
+                                            Datatype, FilterPipeline, PositiveDeltaFilter)
+    dd = CompressionFilter(Compressor.DOUBLE_DELTA, -1)
+    rle = CompressionFilter(Compressor.RLE, -1)
+    P = lambda *f: FilterPipeline(65536, list(f)).serialize()  # noqa: E731
+    table = {
+        "c1": (P(ByteshuffleFilter()), Datatype.INT32, 4, c1_values, c1_tile),
+        "c2": (P(BitshuffleFilter(), BitWidthReductionFilter(256)), Datatype.FLOAT32, 4,
+               lambda var, k, rng: c2_values(k, rng), lambda v: c2_tile(v, False)),
+        "c2i": (P(BitshuffleFilter(), BitWidthReductionFilter(256)), Datatype.INT32, 4,
+                lambda var, k, rng: c2_values(k, rng), lambda v: c2_tile(v, True)),
+        "c3a": (P(dd), Datatype.UINT64, 8, lambda var, k, rng: c3_values(k, rng), c3a_tile),
+        "c3b": (P(rle), Datatype.UINT64, 8, lambda var, k, rng: c3_values(k, rng), c3b_tile),
+        "c4": (P(PositiveDeltaFilter(1024), BitWidthReductionFilter(256)), Datatype.UINT64, 8,
+               lambda var, k, rng: c4_values(k, rng), c4_tile),
+        "c5": (c5_pipeline_bytes(), Datatype.INT32, 4, c5_values, c5_filter_tile),
+    }
+    return table[name]
+
+
+def pool(name: str, variant: str, nunique: int, seed: int):
+    """nunique distinct on-disk tiles of a config + their unfiltered values."""
+    ser, dt, cs, values, tile = config(name)
+    rng = np.random.default_rng(seed)
+    vals = [values(variant, k, rng) for k in range(nunique)]
+    return [tile(v) for v in vals], vals
 
 
 def c5_values(variant: str, tile_index: int, rng: np.random.Generator) -> np.ndarray:
