@@ -3,7 +3,9 @@
 
 Workload (BASELINE.json configs[4]): dense int32 tiles of
 64 KiB (one chunk each), pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)],
-12,500 tiles per GPU (C5's 100k tiles over 8 GPUs; weak scaling).  A step is
+12,500 tiles per GPU (C5's 100k tiles over 8 GPUs; weak scaling).  The other
+configs run with --config c1|c2|c2i|c3a|c3b|c4 (parity-test cases; not the
+headline line).  A step is
 one unfilter pass (one tdbg_unfilter_tiles_async launch) over the rank's
 12,500 resident tiles.  The headline `value` is the "rand" data variant
 (every byte moves; DD falls back to raw); the "ramp" variant is reported
@@ -27,10 +29,32 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
+# BASELINE.json configs; per-GPU tile counts at the GPU
+# counts the configs name (weak scaling: the same per-GPU work at any N)
+CONFIGS = {
+    "c1": dict(tiles_per_gpu=256, variants="ramp,rand", dtype="int32",
+               workload="C1: 2D int32 dense, [BYTESHUFFLE], 256 tiles x 64 KiB"),
+    "c2": dict(tiles_per_gpu=10000, variants="sin", dtype="float32",
+               workload="C2: dense float32, [BITSHUFFLE, BIT_WIDTH_REDUCTION(256)] (BWR pass-through "
+                        "on float), 10k tiles x 64 KiB"),
+    "c2i": dict(tiles_per_gpu=10000, variants="sin", dtype="int32",
+                workload="C2i: C2's bytes typed INT32 (BWR active), 10k tiles x 64 KiB"),
+    "c3a": dict(tiles_per_gpu=10000, variants="coords", dtype="uint64",
+                workload="C3a: sparse uint64 coords, [DOUBLE_DELTA], 10k tiles x 64 KiB"),
+    "c3b": dict(tiles_per_gpu=10000, variants="coords", dtype="uint64",
+                workload="C3b: sparse uint64 coords, [RLE] (cell 8), 10k tiles x 64 KiB"),
+    "c4": dict(tiles_per_gpu=12500, variants="offsets", dtype="uint64",
+               workload="C4: var-length offsets uint64, [POSITIVE_DELTA(1024), BIT_WIDTH_REDUCTION(256)], "
+                        "50k tiles / 4 GPUs"),
+    "c5": dict(tiles_per_gpu=12500, variants="rand,ramp", dtype="int32",
+               workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
+                        "64 KiB tiles (1 chunk), device-resident, 100k tiles / 8 GPUs"),
+}
 
-def build_batch(engine, variant: str, ntiles: int, nunique: int, device: int, seed: int):
+
+def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, device: int, seed: int):
     import workloads as W
-    pool, vals = W.c5_pool(variant, nunique, seed=seed)
+    pool, vals = W.pool(cfg, variant, nunique, seed)
     idx = np.arange(ntiles) % nunique
     sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
     al = (sizes + np.uint64(15)) // np.uint64(16) * np.uint64(16)
@@ -40,19 +64,20 @@ def build_batch(engine, variant: str, ntiles: int, nunique: int, device: int, se
     pool_np = [np.frombuffer(p, dtype=np.uint8) for p in pool]
     for k, (i, o) in enumerate(zip(idx, offs)):
         packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
-    batch = engine.TileBatch.from_packed(packed, offs, sizes, [W.TILE_BYTES] * ntiles,
-                                         device=device)
+    out_sizes = [vals[i].nbytes for i in idx]
+    batch = engine.TileBatch.from_packed(packed, offs, sizes, out_sizes, device=device)
     return batch, pool, vals, idx, packed, offs, sizes
 
 
 def verify(batch, vals, idx) -> None:
-    out = batch.d_out[: len(idx) * 65536].view(-1, 65536)
+    """Every distinct source tile's first occurrence equals its values."""
     first = {}
     for t, i in enumerate(idx):
         if i not in first:
             first[i] = t
     for i, t in first.items():
-        got = out[t].cpu().numpy()
+        o, n = int(batch.out_off[t]), int(batch.out_size[t])
+        got = batch.d_out[o:o + n].cpu().numpy()
         if not np.array_equal(got, vals[i].view(np.uint8)):
             raise SystemExit(f"bench verification failed: tile {t} differs from its source values")
 
@@ -94,15 +119,17 @@ def max_over_ranks(dist, x: float, device: str) -> float:
     return float(t.item())
 
 
-def cpu_baseline(packed, offs, sizes, ntiles_sample: int, threads: int, min_seconds: float = 10.0):
+def cpu_baseline(cfg, packed, offs, sizes, out_bytes, ntiles_sample: int, threads: int,
+                 min_seconds: float = 10.0):
     """Oracle (CPU restatement, test infrastructure) on a bounded sample."""
     from oracle import oracle as O
     import workloads as W
-    op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+    ser, dt, cs, _, _ = W.config(cfg)
+    op = O.OraclePipeline(ser, 23, int(dt), cs)
     n = min(ntiles_sample, offs.size)
-    out = np.zeros(n * W.TILE_BYTES, dtype=np.uint8)
-    out_off = np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES)
-    out_size = np.full(n, W.TILE_BYTES, dtype=np.uint64)
+    out = np.zeros(n * out_bytes, dtype=np.uint8)
+    out_off = np.arange(n, dtype=np.uint64) * np.uint64(out_bytes)
+    out_size = np.full(n, out_bytes, dtype=np.uint64)
     reps = 0
     t0 = time.perf_counter()
     while True:
@@ -113,7 +140,7 @@ def cpu_baseline(packed, offs, sizes, ntiles_sample: int, threads: int, min_seco
         el = time.perf_counter() - t0
         if el >= min_seconds:
             break
-    gib = reps * n * W.TILE_BYTES / 2**30
+    gib = reps * n * out_bytes / 2**30
     return gib / el, reps * n, el
 
 
@@ -133,9 +160,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--tiles-per-gpu", type=int, default=12500)
+    ap.add_argument("--config", default="c5", choices=sorted(CONFIGS),
+                    help="BASELINE config (default C5, the metric's 3-stage pipeline)")
+    ap.add_argument("--tiles-per-gpu", type=int, default=0,
+                    help="default: the config's per-GPU tile count (C5: 100k / 8)")
     ap.add_argument("--unique", type=int, default=128)
-    ap.add_argument("--variants", default="rand,ramp")
+    ap.add_argument("--variants", default="")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time host-resident end-to-end")
@@ -156,13 +186,16 @@ def main():
     from tiledb_amd import engine
     import workloads as W
 
-    dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)  # INT32, cell 4
+    cfg = CONFIGS[args.config]
+    ntiles = args.tiles_per_gpu or cfg["tiles_per_gpu"]
+    ser, dt, cs, _, _ = W.config(args.config)
+    dp = engine.DevicePipeline(ser, 23, int(dt), cs)
     ctx = engine.Context(local)
-    variants = [v for v in args.variants.split(",") if v]
+    variants = [v for v in (args.variants or cfg["variants"]).split(",") if v]
     res = {}
     for vi, var in enumerate(variants):
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
-            engine, var, args.tiles_per_gpu, args.unique, local, seed=5 + 1000 * rank + vi)
+            engine, args.config, var, ntiles, args.unique, local, seed=5 + 1000 * rank + vi)
         ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
         if not os.environ.get("TDBG_DEBUG_STOP"):  # timing-only ablation skips output checks
             verify(batch, vals, idx)
@@ -172,10 +205,11 @@ def main():
         # (every tile a view tile), else the fused LDS kernel
         kname, kern_ms = (("unfilter_view_kernel", view_ms) if view_ms >= fused_ms
                           else ("unfilter_fused_kernel", fused_ms))
-        unf = float(args.tiles_per_gpu) * W.TILE_BYTES
+        unf = float(sum(vals[i].nbytes for i in idx))
         b_alg = float(sizes.sum()) + unf
         res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, kname=kname, view_ms=view_ms,
                         fused_ms=fused_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
+                        out_bytes=int(vals[0].nbytes),
                         packed=packed, offs=offs, sizes=sizes)
         if args.e2e:
             res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, args)
@@ -188,7 +222,7 @@ def main():
     total_unf = r["unf"] * world
     value = total_unf / (r["elapsed"] / args.steps) / 2**30
     achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
-    traffic = load_traffic(head)
+    traffic = load_traffic(head) if args.config == "c5" else None
     line = {
         "metric": "GiB/s unfiltered tile bytes (device-resident), 64 KiB chunks, 3-stage pipeline",
         "value": round(value, 2),
@@ -200,12 +234,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
-        "data": f"synthetic C5 '{head}' tiles ({args.unique} unique, replicated), numpy-encoded",
+        "dtype": cfg["dtype"],
+        "data": f"synthetic {args.config.upper()} '{head}' tiles ({args.unique} unique, replicated), "
+                "numpy-encoded (workloads.py)",
         "config": {
-            "workload": "C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
-                        "64 KiB tiles (1 chunk), device-resident",
-            "tiles_per_gpu": args.tiles_per_gpu,
+            "workload": cfg["workload"],
+            "tiles_per_gpu": ntiles,
             "variant": head,
             "parallelism": f"tile-shard x{world} (no collectives)",
             "filtered_bytes_per_gpu": int(r["sizes"].sum()),
@@ -235,13 +269,14 @@ def main():
         line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        cpu, ntl, el = cpu_baseline(r["packed"], r["offs"], r["sizes"], 2048, threads)
+        cpu, ntl, el = cpu_baseline(args.config, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
+                                    2048, threads)
         line["cpu_baseline"] = {
             "value": round(cpu, 3),
             "unit": "GiB/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"{ntl} C5 '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s on "
+            "sample": f"{ntl} {args.config.upper()} '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s on "
                       f"{threads} threads, oracle/ C restatement",
         }
     if rank == 0:

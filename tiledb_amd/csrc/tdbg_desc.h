@@ -62,6 +62,7 @@ struct KParams {
   uint32_t slot_cap, md_cap, tab_cap;
   uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
   uint32_t fixup;     // general kernel: only the tiles queued in fbq (TDBG_E_FALLBACK)
+  uint32_t dbg_print; // diagnostics: block 0 prints its progress (TDBG_DEBUG_PRINT)
   // Fallback queue of this launch: fbq[0] = count, fbq[1 + k] = tile index.
   // The fused kernel appends the tiles it declines; the fixup launch walks
   // the queue and clears fbq_next[0], the queue the context's next launch

@@ -1444,6 +1444,9 @@ unfilter_fused_kernel(const KParams kp) {
     ntl = __builtin_amdgcn_readfirstlane(kp.ldsq[0]);
     tl = kp.ldsq + 1;
   }
+  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2)
+    printf("fused b%u: ntl %llu ldsq %p ntiles %llu\n", (unsigned)blockIdx.x, (unsigned long long)ntl,
+           (void*)kp.ldsq, (unsigned long long)kp.ntiles);
   TileDesc dn{};
   if (blockIdx.x < ntl) {
     dn = desc_uniform(desc_load(kp, tl, blockIdx.x));
@@ -1549,6 +1552,7 @@ unfilter_fused_kernel(const KParams kp) {
     }
     pc.mark(6);
   }
+  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2) printf("fused b%u: done\n", (unsigned)blockIdx.x);
   pc.flush();
 }
 

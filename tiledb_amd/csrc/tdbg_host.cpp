@@ -464,6 +464,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   {
     static const char* dbg = getenv("TDBG_DEBUG_STOP");  // timing-only ablation
     kp.dbg_stop = dbg ? (uint32_t)atoi(dbg) : 0;
+    static const char* dbg_print = getenv("TDBG_DEBUG_PRINT");
+    kp.dbg_print = dbg_print ? (uint32_t)atoi(dbg_print) : 0u;
   }
   const bool fast = !force_general && p->plan.fast != 0;
   uint32_t grid;
@@ -512,22 +514,34 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   HIP_OK(hipEventRecord(c->ev0, stream));
   if (te) HIP_OK(hipEventRecord(te[0], stream));
   hipError_t e;
+  static const bool skip_view_kernel = getenv("TDBG_DEBUG_SKIP_VIEW_KERNEL") != nullptr;
   if (view) {
     kp.ldsq = c->d_ldsq[c->fbq_parity ^ 1];  // this launch's queue (parity flipped above)
-    e = tdbg_launch_view(&kp, (uint32_t)c->cus * 8, stream);
+    e = skip_view_kernel ? hipSuccess : tdbg_launch_view(&kp, (uint32_t)c->cus * 8, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("view launch: ") + hipGetErrorString(e));
   }
   if (te) HIP_OK(hipEventRecord(te[1], stream));
   static const bool view_only = getenv("TDBG_DEBUG_VIEW_ONLY") != nullptr;  // diagnostics
+  static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;
+  static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;
   if (view && view_only) {
     HIP_OK(hipEventRecord(c->ev1, stream));
     c->timed = true;
     return TDBG_OK;
   }
-  e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
+  static const bool sync_after_view = getenv("TDBG_DEBUG_SYNC_AFTER_VIEW") != nullptr;
+  if (view && sync_after_view) HIP_OK(hipStreamSynchronize(stream));
+  static const bool event_after_view = getenv("TDBG_DEBUG_EVENT_AFTER_VIEW") != nullptr;
+  if (view && event_after_view) HIP_OK(hipEventRecord(c->ev1, stream));
+  static const bool fused_empty = getenv("TDBG_DEBUG_FUSED_EMPTY") != nullptr;
+  if (view && fused_empty) {
+    kp.ldsq = nullptr;
+    kp.ntiles = 0;
+  }
+  if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
   if (te) HIP_OK(hipEventRecord(te[2], stream));
-  if (queued) {
+  if (queued && !skip_fixup) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
     // with an empty queue every workgroup exits after one load
@@ -668,6 +682,17 @@ int tdbg_context_launch_times(tdbg_context* c, float* view_ms, float* kernel_ms,
   *count = n;
   c->tcap = 0;  // disarm
   c->tcount = 0;
+  return TDBG_OK;
+}
+
+extern "C" int tdbg_debug_queue_counts(tdbg_context* c, uint32_t* out4) {
+  if (!c || !out4) return fail(TDBG_E_ARG, "null argument");
+  HIP_OK(hipDeviceSynchronize());
+  for (int k = 0; k < 2; k++) {
+    out4[k] = out4[2 + k] = 0xffffffffu;
+    if (c->d_fbq[k]) HIP_OK(hipMemcpy(&out4[k], c->d_fbq[k], 4, hipMemcpyDeviceToHost));
+    if (c->d_ldsq[k]) HIP_OK(hipMemcpy(&out4[2 + k], c->d_ldsq[k], 4, hipMemcpyDeviceToHost));
+  }
   return TDBG_OK;
 }
 

@@ -45,9 +45,25 @@ typedef __attribute__((address_space(1))) const uint8_t vg_cu8;
 typedef __attribute__((address_space(1))) v4u vg_u4;
 typedef __attribute__((address_space(1))) uint8_t vg_u8;
 
-// Unaligned global loads (gfx950 runs HSA queues in unaligned access mode).
-__device__ __forceinline__ uint32_t u32at(const uint8_t* p) { return *(vg_cu32*)p; }
-__device__ __forceinline__ uint32_t u16at(const uint8_t* p) { return *(vg_cu16*)p; }
+// Global loads at arbitrary byte offsets, built from naturally aligned dword
+// loads (two per value; both hit the same or adjacent cache lines) and
+// v_alignbyte.  Only the dwords that hold requested bytes are read.
+__device__ __forceinline__ uint32_t u32at(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const vg_cu32* q = (const vg_cu32*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t lo = q[0];
+  const uint32_t hi = sh ? q[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__device__ __forceinline__ uint32_t u16at(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const vg_cu32* q = (const vg_cu32*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t lo = q[0];
+  const uint32_t hi = sh == 3 ? q[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh) & 0xffffu;
+}
 __device__ __forceinline__ uint32_t u8at(const uint8_t* p) { return *(vg_cu8*)p; }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
@@ -190,7 +206,7 @@ __device__ __forceinline__ uint32_t unshuf_at(const uint8_t* s, uint32_t n, uint
 }
 
 template <int TS>
-__device__ __forceinline__ void view_slice(const ViewSrc& v, uint8_t* out, uint32_t q) {
+__device__ __forceinline__ void view_slice(const ViewSrc& v, uint8_t* out, uint32_t q, bool plain) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n = v.n, N = n / TS;
   const uint32_t b0 = q * VSLICE, b1 = n < b0 + VSLICE ? n : b0 + VSLICE;
@@ -209,7 +225,10 @@ __device__ __forceinline__ void view_slice(const ViewSrc& v, uint8_t* out, uint3
 #pragma unroll
     for (int s = 0; s < VSTEPS; s++) {
       const uint32_t k = kb + s * 64 + lane;
-      if (k < k1) __builtin_nontemporal_store(unit_mix<TS>(r[s]), (vg_u4*)(out + 16 * k));
+      if (k < k1) {
+        if (plain) *(vg_u4*)(out + 16 * k) = unit_mix<TS>(r[s]);
+        else __builtin_nontemporal_store(unit_mix<TS>(r[s]), (vg_u4*)(out + 16 * k));
+      }
     }
   }
   for (uint32_t o = (k1 > k0 ? 16 * k1 : b0) + lane; o < b1; o += 64)
@@ -222,6 +241,9 @@ __global__ void __launch_bounds__(VNT) unfilter_view_kernel(const KParams kp) {
   const uint64_t wid = (uint64_t)blockIdx.x * (VNT / 64) + (threadIdx.x >> 6);
   const uint64_t nwv = (uint64_t)gridDim.x * (VNT / 64);
   const uint64_t nu = kp.ntiles * VSLICES;
+  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2)
+    printf("view b%u: nu %llu nwv %llu wid %llu\n", (unsigned)blockIdx.x, (unsigned long long)nu,
+           (unsigned long long)nwv, (unsigned long long)wid);
   for (uint64_t u = wid; u < nu; u += nwv) {
     const uint64_t t = u / VSLICES;
     const uint32_t q = (uint32_t)(u % VSLICES);
@@ -242,8 +264,9 @@ __global__ void __launch_bounds__(VNT) unfilter_view_kernel(const KParams kp) {
       continue;
     }
     if (q == 0 && lane == 0 && kp.status) kp.status[t] = TDBG_OK;
-    view_slice<TS>(v, out, q);
+    view_slice<TS>(v, out, q, (kp.dbg_print & 2) != 0);
   }
+  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2) printf("view b%u: done\n", (unsigned)blockIdx.x);
 }
 
 }  // namespace tdbg
