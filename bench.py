@@ -105,10 +105,10 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    view_ms, kern_ms, total_ms = ctx.launch_times(steps)
+    kern_ms, total_ms = ctx.launch_times(steps)
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, "cuda")
-    return elapsed, float(np.mean(view_ms)), float(np.mean(kern_ms)), float(np.mean(total_ms))
+    return elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms))
 
 
 def max_over_ranks(dist, x: float, device: str) -> float:
@@ -199,16 +199,12 @@ def main():
         ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
         if not os.environ.get("TDBG_DEBUG_STOP"):  # timing-only ablation skips output checks
             verify(batch, vals, idx)
-        elapsed, view_ms, fused_ms, launch_ms = time_device(engine, ctx, dp, batch, args.steps,
-                                                            args.warmup, dist, world)
-        # the dominant kernel: the streaming view kernel when it did the work
-        # (every tile a view tile), else the fused LDS kernel
-        kname, kern_ms = (("unfilter_view_kernel", view_ms) if view_ms >= fused_ms
-                          else ("unfilter_fused_kernel", fused_ms))
+        elapsed, kern_ms, launch_ms = time_device(engine, ctx, dp, batch, args.steps,
+                                                  args.warmup, dist, world)
+        kname = "unfilter_fused_kernel"
         unf = float(sum(vals[i].nbytes for i in idx))
         b_alg = float(sizes.sum()) + unf
-        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, kname=kname, view_ms=view_ms,
-                        fused_ms=fused_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
+        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, kname=kname, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
                         out_bytes=int(vals[0].nbytes),
                         packed=packed, offs=offs, sizes=sizes)
         if args.e2e:
@@ -253,8 +249,6 @@ def main():
             "traffic": traffic,
             "kernel": r["kname"],
             "kernel_ms": round(r["kern_ms"], 4),
-            "view_kernel_ms": round(r["view_ms"], 4),
-            "fused_kernel_ms": round(r["fused_ms"], 4),
             "launch_ms": round(r["launch_ms"], 4),
             "algorithmic_bytes_per_launch": int(r["b_alg"]),
         },

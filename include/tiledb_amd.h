@@ -211,15 +211,13 @@ int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
 
 /* Per-launch device timing for benchmarks: arm event recording for the next
  * n tdbg_unfilter_tiles_* launches on ctx, then read them back (waits for the
- * last armed launch).  A launch is up to three kernels on one stream: the
- * streaming view kernel (byteshuffle[-DD][-BWR] pipelines), the fused LDS
- * kernel (or the general kernel), the fallback fixup.  view_ms[i] = the view
- * kernel of launch i (0 if none ran), kernel_ms[i] = the fused/general
- * kernel, total_ms[i] = all of the launch.  Outputs may be NULL; reading
- * disarms. */
+ * last armed launch).  A launch is up to two kernels on one stream: the
+ * fused LDS kernel (or the general kernel), then the fallback fixup.
+ * kernel_ms[i] = the fused/general kernel of launch i, total_ms[i] = all of
+ * the launch.  Outputs may be NULL; reading disarms. */
 int tdbg_context_time_launches(tdbg_context* ctx, uint32_t n);
-int tdbg_context_launch_times(tdbg_context* ctx, float* view_ms, float* kernel_ms,
-                              float* total_ms, uint32_t cap, uint32_t* count);
+int tdbg_context_launch_times(tdbg_context* ctx, float* kernel_ms, float* total_ms,
+                              uint32_t cap, uint32_t* count);
 
 /* Diagnostics (no reference counterpart): with TDBG_PROF=1 in the
  * environment, the fused kernel accumulates shader-clock cycles per phase

@@ -264,21 +264,21 @@ def edge_cases() -> List[Case]:
     # tile sizes 1 and 0
     cases.append(Case("one_byte_tile", P(ByteshuffleFilter()), Datatype.UINT8, 1,
                       [np.array([42], dtype=np.uint8)]))
-    # streaming view kernel (tdbg_view.hip): incompressible C1/C5 shapes at
-    # every element width, ragged sizes (16-B unit tails, plane tails, tiles
-    # under one 16 KiB slice), unaligned outputs (ragged tiles packed back to
-    # back), mixed view / non-view tiles in one batch, offsets tiles
+    # incompressible C1/C5 shapes (every stage before the byteshuffle takes
+    # its raw path) at every element width, ragged sizes (16-B unit tails,
+    # plane tails), unaligned outputs (ragged tiles packed back to back),
+    # raw and compressed tiles mixed in one batch, offsets tiles
     c5p = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
     for dt, n in ((Datatype.INT16, 32768), (Datatype.INT32, 16383), (Datatype.INT64, 8191),
                   (Datatype.INT32, 1000), (Datatype.UINT16, 32767)):
         sz = datatype_size(dt)
         tiles = [rng.integers(0, 256, n * sz, dtype=np.uint8) for _ in range(3)]
-        cases.append(Case(f"view_c5_rand_{dt.name}_{n}", c5p, dt, sz, tiles))
-        cases.append(Case(f"view_c1_rand_{dt.name}_{n}", P(ByteshuffleFilter()), dt, sz, tiles))
+        cases.append(Case(f"incomp_c5_rand_{dt.name}_{n}", c5p, dt, sz, tiles))
+        cases.append(Case(f"incomp_c1_rand_{dt.name}_{n}", P(ByteshuffleFilter()), dt, sz, tiles))
     mixed = [rng.integers(0, 256, 65536, dtype=np.uint8), as_u8(np.arange(16384, dtype=np.int32)),
              rng.integers(0, 256, 65532, dtype=np.uint8), as_u8(np.arange(16383, dtype=np.int32) * 7)]
-    cases.append(Case("view_c5_mixed_view_and_lds", c5p, I32, 4, mixed))
-    cases.append(Case("view_c5_offsets_u64", c5p, U64, 8,
+    cases.append(Case("incomp_c5_mixed_raw_and_packed", c5p, I32, 4, mixed))
+    cases.append(Case("incomp_c5_offsets_u64", c5p, U64, 8,
                       [rng.integers(0, 256, 8 * 8191, dtype=np.uint8)], offsets_tile=True))
     return cases
 

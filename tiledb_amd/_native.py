@@ -53,7 +53,7 @@ SIGNATURES = {
     "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "tdbg_context_time_launches": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
-    "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint32,
+    "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint32,
                                                  ctypes.POINTER(ctypes.c_uint32)]),
     "tdbg_debug_phase_clocks": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]),
     "tdbg_shard_tiles": (ctypes.c_int, [ctypes.c_uint64, c_vp, c_vp, ctypes.c_uint32, c_vp]),

@@ -18,8 +18,7 @@ ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 
 NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART_HOST)
 # (source, object name, extra flags)
-UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_view.hip", "tdbg_view", []),
-          ("tdbg_host.cpp", "tdbg_host", [])] +
+UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_host.cpp", "tdbg_host", [])] +
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
 HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h"]

@@ -34,7 +34,6 @@ struct tdbg_stage {
 struct tdbg_plan {
   uint32_t nstages;
   uint32_t fast;  // fused fast-path selector (tdbg_fast_kind), 0 = none
-  uint32_t view;  // streaming view-kernel selector (tdbg_view.hip), 0 = none
   tdbg_stage s[TDBG_MAX_FILTERS];
 };
 
@@ -62,18 +61,12 @@ struct KParams {
   uint32_t slot_cap, md_cap, tab_cap;
   uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
   uint32_t fixup;     // general kernel: only the tiles queued in fbq (TDBG_E_FALLBACK)
-  uint32_t dbg_print; // diagnostics: block 0 prints its progress (TDBG_DEBUG_PRINT)
   // Fallback queue of this launch: fbq[0] = count, fbq[1 + k] = tile index.
   // The fused kernel appends the tiles it declines; the fixup launch walks
   // the queue and clears fbq_next[0], the queue the context's next launch
   // appends to (two queues alternate per launch on the context's stream).
   uint32_t* fbq;
   uint32_t* fbq_next;
-  // LDS queue (same layout as fbq): the view kernel appends the tiles it
-  // cannot stream; the fused kernel, when ldsq is set, walks that queue
-  // instead of all ntiles.  ldsq_next[0] is cleared by the fixup launch.
-  uint32_t* ldsq;
-  uint32_t* ldsq_next;
   uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
   tdbg_plan plan;
 };

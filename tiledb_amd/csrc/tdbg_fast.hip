@@ -26,8 +26,6 @@
 namespace tdbg {
 
 constexpr int FNT = 512;             // threads per workgroup
-constexpr int FP = 192;              // bytes of stage output per thread (slice)
-constexpr int FPD = FP / 4;          // dwords per slice
 constexpr uint32_t XCAP = 66048;     // in-place data buffer (64.5 KiB)
 constexpr uint32_t MDCAP = 4608;     // chunk metadata / decompressed metadata
 constexpr uint32_t TABN = 512;       // per-window table entries (uint4)
@@ -1437,16 +1435,9 @@ unfilter_fused_kernel(const KParams kp) {
   pf.cnt = 0;
   pf.base = 0;
   constexpr bool PF = pf_enabled(S0, S1, S2, S3);
-  // tiles: all ntiles, a host-given list (retry), or the view kernel's queue
-  uint64_t ntl = kp.ntiles;
+  // tiles: all ntiles, or a host-given list (the sync entry's retry)
+  const uint64_t ntl = kp.ntiles;
   const uint32_t* tl = kp.tile_list;
-  if (kp.ldsq) {
-    ntl = __builtin_amdgcn_readfirstlane(kp.ldsq[0]);
-    tl = kp.ldsq + 1;
-  }
-  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2)
-    printf("fused b%u: ntl %llu ldsq %p ntiles %llu\n", (unsigned)blockIdx.x, (unsigned long long)ntl,
-           (void*)kp.ldsq, (unsigned long long)kp.ntiles);
   TileDesc dn{};
   if (blockIdx.x < ntl) {
     dn = desc_uniform(desc_load(kp, tl, blockIdx.x));
@@ -1552,7 +1543,6 @@ unfilter_fused_kernel(const KParams kp) {
     }
     pc.mark(6);
   }
-  if ((kp.dbg_print & 1) && threadIdx.x == 0 && blockIdx.x < 2) printf("fused b%u: done\n", (unsigned)blockIdx.x);
   pc.flush();
 }
 

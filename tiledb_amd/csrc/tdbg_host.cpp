@@ -27,8 +27,6 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
                                           hipStream_t stream);
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
-extern "C" hipError_t tdbg_launch_view(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
-extern "C" uint32_t tdbg_view_select(const tdbg_plan* plan);
 #define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
 #define TDBG_DECL_PART(k) \
   extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
@@ -123,7 +121,6 @@ struct tdbg_context {
   uint64_t list_cap = 0;
   // fused-kernel fallback queues (KParams::fbq), alternating per launch
   uint32_t* d_fbq[2] = {nullptr, nullptr};
-  uint32_t* d_ldsq[2] = {nullptr, nullptr};  // view kernel -> fused kernel queues (KParams::ldsq)
   uint32_t fbq_parity = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -173,14 +170,13 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   if (c->d_need) HIP_OK(hipFree(c->d_need));
   HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
   HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
-  for (uint32_t** qs : {c->d_fbq, c->d_ldsq})
-    for (int k = 0; k < 2; k++) {
-      uint32_t*& q = qs[k];
-      if (q) HIP_OK(hipFree(q));
-      q = nullptr;
-      HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
-      HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
-    }
+  for (int k = 0; k < 2; k++) {
+    uint32_t*& q = c->d_fbq[k];
+    if (q) HIP_OK(hipFree(q));
+    q = nullptr;
+    HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
+    HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
+  }
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -270,7 +266,6 @@ void build_plan(tdbg_pipeline* p) {
     }
   }
   P.fast = p->supported ? tdbg_fast_select(&P) : 0;
-  P.view = P.fast ? tdbg_view_select(&P) : 0;
 }
 
 }  // namespace
@@ -422,8 +417,6 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_list) (void)hipFree(c->d_list);
   for (auto* q : c->d_fbq)
     if (q) (void)hipFree(q);
-  for (auto* q : c->d_ldsq)
-    if (q) (void)hipFree(q);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -464,8 +457,6 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   {
     static const char* dbg = getenv("TDBG_DEBUG_STOP");  // timing-only ablation
     kp.dbg_stop = dbg ? (uint32_t)atoi(dbg) : 0;
-    static const char* dbg_print = getenv("TDBG_DEBUG_PRINT");
-    kp.dbg_print = dbg_print ? (uint32_t)atoi(dbg_print) : 0u;
   }
   const bool fast = !force_general && p->plan.fast != 0;
   uint32_t grid;
@@ -499,48 +490,20 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     }
   }
   const bool queued = fast && d_status && !kp.dbg_stop;
-  // streaming view kernel first (tdbg_view.hip) when the pipeline has the
-  // byteshuffle[-DD][-BWR] shape; it queues non-view tiles for the fused kernel
-  // (opt-in while the streaming path is being validated on hardware)
-  static const bool use_view = getenv("TDBG_VIEW") != nullptr && getenv("TDBG_NO_VIEW") == nullptr;
-  const bool view = queued && !d_list && p->plan.view != 0 && use_view;
   if (queued) {
     kp.fbq = c->d_fbq[c->fbq_parity];
     kp.fbq_next = c->d_fbq[c->fbq_parity ^ 1];
-    kp.ldsq_next = c->d_ldsq[c->fbq_parity ^ 1];
     c->fbq_parity ^= 1;
   }
-  hipEvent_t* te = c->tcount < c->tcap ? &c->tev[4 * c->tcount++] : nullptr;
+  hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   HIP_OK(hipEventRecord(c->ev0, stream));
   if (te) HIP_OK(hipEventRecord(te[0], stream));
-  hipError_t e;
-  static const bool skip_view_kernel = getenv("TDBG_DEBUG_SKIP_VIEW_KERNEL") != nullptr;
-  if (view) {
-    kp.ldsq = c->d_ldsq[c->fbq_parity ^ 1];  // this launch's queue (parity flipped above)
-    e = skip_view_kernel ? hipSuccess : tdbg_launch_view(&kp, (uint32_t)c->cus * 8, stream);
-    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("view launch: ") + hipGetErrorString(e));
-  }
-  if (te) HIP_OK(hipEventRecord(te[1], stream));
-  static const bool view_only = getenv("TDBG_DEBUG_VIEW_ONLY") != nullptr;  // diagnostics
-  static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;
-  static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;
-  if (view && view_only) {
-    HIP_OK(hipEventRecord(c->ev1, stream));
-    c->timed = true;
-    return TDBG_OK;
-  }
-  static const bool sync_after_view = getenv("TDBG_DEBUG_SYNC_AFTER_VIEW") != nullptr;
-  if (view && sync_after_view) HIP_OK(hipStreamSynchronize(stream));
-  static const bool event_after_view = getenv("TDBG_DEBUG_EVENT_AFTER_VIEW") != nullptr;
-  if (view && event_after_view) HIP_OK(hipEventRecord(c->ev1, stream));
-  static const bool fused_empty = getenv("TDBG_DEBUG_FUSED_EMPTY") != nullptr;
-  if (view && fused_empty) {
-    kp.ldsq = nullptr;
-    kp.ntiles = 0;
-  }
+  hipError_t e = hipSuccess;
+  static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
+  static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
   if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
-  if (te) HIP_OK(hipEventRecord(te[2], stream));
+  if (te) HIP_OK(hipEventRecord(te[1], stream));
   if (queued && !skip_fixup) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
@@ -551,7 +514,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
   }
   HIP_OK(hipEventRecord(c->ev1, stream));
-  if (te) HIP_OK(hipEventRecord(te[3], stream));
+  if (te) HIP_OK(hipEventRecord(te[2], stream));
   c->timed = true;
   return TDBG_OK;
 }
@@ -658,7 +621,7 @@ int tdbg_context_stats(const tdbg_context* c, uint64_t* tiles, uint64_t* bytes) 
 int tdbg_context_time_launches(tdbg_context* c, uint32_t n) {
   if (!c) return fail(TDBG_E_ARG, "null context");
   HIP_OK(hipSetDevice(c->device));
-  while (c->tev.size() < 4ull * n) {
+  while (c->tev.size() < 3ull * n) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     c->tev.push_back(e);
@@ -668,31 +631,19 @@ int tdbg_context_time_launches(tdbg_context* c, uint32_t n) {
   return TDBG_OK;
 }
 
-int tdbg_context_launch_times(tdbg_context* c, float* view_ms, float* kernel_ms, float* total_ms,
-                              uint32_t cap, uint32_t* count) {
+int tdbg_context_launch_times(tdbg_context* c, float* kernel_ms, float* total_ms, uint32_t cap,
+                              uint32_t* count) {
   if (!c || !count) return fail(TDBG_E_ARG, "null argument");
   const uint32_t n = std::min(c->tcount, cap);
   for (uint32_t i = 0; i < n; i++) {
-    hipEvent_t* e = &c->tev[4 * i];
-    HIP_OK(hipEventSynchronize(e[3]));
-    if (view_ms) HIP_OK(hipEventElapsedTime(&view_ms[i], e[0], e[1]));
-    if (kernel_ms) HIP_OK(hipEventElapsedTime(&kernel_ms[i], e[1], e[2]));
-    if (total_ms) HIP_OK(hipEventElapsedTime(&total_ms[i], e[0], e[3]));
+    hipEvent_t* e = &c->tev[3 * i];
+    HIP_OK(hipEventSynchronize(e[2]));
+    if (kernel_ms) HIP_OK(hipEventElapsedTime(&kernel_ms[i], e[0], e[1]));
+    if (total_ms) HIP_OK(hipEventElapsedTime(&total_ms[i], e[0], e[2]));
   }
   *count = n;
   c->tcap = 0;  // disarm
   c->tcount = 0;
-  return TDBG_OK;
-}
-
-extern "C" int tdbg_debug_queue_counts(tdbg_context* c, uint32_t* out4) {
-  if (!c || !out4) return fail(TDBG_E_ARG, "null argument");
-  HIP_OK(hipDeviceSynchronize());
-  for (int k = 0; k < 2; k++) {
-    out4[k] = out4[2 + k] = 0xffffffffu;
-    if (c->d_fbq[k]) HIP_OK(hipMemcpy(&out4[k], c->d_fbq[k], 4, hipMemcpyDeviceToHost));
-    if (c->d_ldsq[k]) HIP_OK(hipMemcpy(&out4[2 + k], c->d_ldsq[k], 4, hipMemcpyDeviceToHost));
-  }
   return TDBG_OK;
 }
 

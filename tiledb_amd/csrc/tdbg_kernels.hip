@@ -64,10 +64,7 @@ unfilter_general_kernel(const KParams kp) {
 __global__ void __launch_bounds__(GEN_NT)
 unfilter_fixup_kernel(const KParams kp) {
   const uint32_t queued = kp.fbq[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    kp.fbq_next[0] = 0;
-    if (kp.ldsq_next) kp.ldsq_next[0] = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) kp.fbq_next[0] = 0;
   if (queued == 0) return;
   const KParams local = kp;  // copied only past the early exit
   general_body(local);

@@ -191,17 +191,15 @@ class Context:
         _check(lib.tdbg_context_time_launches(self.h, n), "tdbg_context_time_launches")
 
     def launch_times(self, cap: int = 4096):
-        """(view_ms, kernel_ms, total_ms) per armed launch: the streaming view
-        kernel, the fused/general kernel, and the whole launch incl. the
-        fallback fixup (waits for the last armed launch)."""
-        v = np.zeros(cap, dtype=np.float32)
+        """(kernel_ms, total_ms) per armed launch: the fused/general kernel and
+        the whole launch incl. the fallback fixup (waits for the last armed launch)."""
         k = np.zeros(cap, dtype=np.float32)
         t = np.zeros(cap, dtype=np.float32)
         n = ctypes.c_uint32()
-        _check(lib.tdbg_context_launch_times(self.h, v.ctypes.data, k.ctypes.data, t.ctypes.data,
+        _check(lib.tdbg_context_launch_times(self.h, k.ctypes.data, t.ctypes.data,
                                              cap, ctypes.byref(n)), "tdbg_context_launch_times")
         m = n.value
-        return v[:m].copy(), k[:m].copy(), t[:m].copy()
+        return k[:m].copy(), t[:m].copy()
 
     def phase_clocks(self, nphases: int = 8) -> np.ndarray:
         """Diagnostics: fused-kernel cycles per phase of the last launch (TDBG_PROF=1)."""
