@@ -168,7 +168,12 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--e2e", action="store_true", help="also time host-resident end-to-end")
+    ap.add_argument("--e2e", action="store_true", default=True,
+                    help="also time host-resident end-to-end (default on; every rank, "
+                         "total over ranks / max-over-ranks time)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    ap.add_argument("--e2e-batch-mb", type=int, default=64,
+                    help="host E2E staging batch (MiB per side; 2 batches in flight)")
     args = ap.parse_args()
 
     import torch
@@ -208,7 +213,7 @@ def main():
                         out_bytes=int(vals[0].nbytes),
                         packed=packed, offs=offs, sizes=sizes)
         if args.e2e:
-            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, args)
+            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, args, dist, world)
         del batch
         torch.cuda.empty_cache()
 
@@ -279,8 +284,10 @@ def main():
         dist.destroy_process_group()
 
 
-def e2e(engine, ctx, dp, packed, offs, sizes, args):
-    """Host-resident end-to-end: pinned H2D + unfilter + D2H (PCIe-inclusive)."""
+def e2e(engine, ctx, dp, packed, offs, sizes, args, dist=None, world=1):
+    """Host-resident end-to-end: pinned H2D + unfilter + D2H (PCIe-inclusive).
+    Every rank moves its own tiles through its own GPU's link; the rate is the
+    total over ranks / the slowest rank's time (not `value`: DESIGN.md)."""
     import torch
     import workloads as W
     n = offs.size
@@ -289,14 +296,19 @@ def e2e(engine, ctx, dp, packed, offs, sizes, args):
     in_ptrs = offs + np.uint64(hin.data_ptr())
     out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES) + np.uint64(hout.data_ptr())
     osz = np.full(n, W.TILE_BYTES, dtype=np.uint64)
-    ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=256 << 20)
+    bb = args.e2e_batch_mb << 20
+    ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=bb)
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     reps = 3
     for _ in range(reps):
-        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=256 << 20)
+        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=bb)
     el = time.perf_counter() - t0
     assert not st.any()
-    return round(reps * n * W.TILE_BYTES / el / 2**30, 2)
+    if dist is not None:
+        el = max_over_ranks(dist, el, "cuda")
+    return round(world * reps * n * W.TILE_BYTES / el / 2**30, 2)
 
 
 if __name__ == "__main__":

@@ -198,6 +198,45 @@ def test_host_end_to_end_and_multi_gpu(eng, ctx, oracle_mod):
         assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
 
 
+def test_host_end_to_end_padded_layouts(eng, ctx, oracle_mod):
+    """Host tiles with alignment padding (coalesced H2D incl. padding), a
+    large gap and an out-of-order tile (separate copies), and padded outputs
+    whose padding bytes must survive the D2H untouched."""
+    import torch
+    case = _CONFIG[-1]
+    _, enc = encode(oracle_mod, case)
+    filtered = [e[0] for e in enc] * 6
+    origs = [e[1] for e in enc] * 6
+    n = len(filtered)
+    sizes = np.array([f.size for f in filtered], dtype=np.uint64)
+    gaps = np.array([(16 - int(s) % 16) % 16 for s in sizes], dtype=np.uint64)
+    gaps[n // 3] = 4096  # too large to copy across
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(sizes + gaps)[:-1]
+    # swap two tiles' host positions: tile 5 lies before tile 4
+    perm_offs = offs.copy()
+    span = int((sizes + gaps).sum())
+    perm_offs[5], perm_offs[4] = span, span + int(sizes[5]) + 8
+    hin = torch.full((span + 512 + int(sizes.max()) * 2,), 0x5A, dtype=torch.uint8).pin_memory()
+    hin_np = hin.numpy()
+    for f, o in zip(filtered, perm_offs):
+        hin_np[int(o):int(o) + f.size] = f
+    osz = np.array([e[2] for e in enc] * 6, dtype=np.uint64)
+    ooff = np.zeros_like(osz)
+    ooff[1:] = np.cumsum(osz + np.uint64(32))[:-1]
+    hout = torch.full((int(ooff[-1] + osz[-1]) + 32,), 0xAB, dtype=torch.uint8).pin_memory()
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    st = ctx.unfilter_host(dp, perm_offs + np.uint64(hin.data_ptr()), sizes,
+                           ooff + np.uint64(hout.data_ptr()), osz, batch_bytes=5 * 65536)
+    assert not st.any()
+    res = hout.numpy()
+    mask = np.ones(res.size, dtype=bool)
+    for i, o in enumerate(origs):
+        assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
+        mask[int(ooff[i]):int(ooff[i]) + int(osz[i])] = False
+    assert (res[mask] == 0xAB).all()
+
+
 def test_async_api_and_timing(eng, ctx, oracle_mod):
     import torch
     case = _CONFIG[0]

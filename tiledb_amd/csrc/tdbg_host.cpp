@@ -139,10 +139,12 @@ struct tdbg_context {
     void* d_ptrs = nullptr;
     int32_t* h_status = nullptr;
     int32_t* d_stat = nullptr;
-    hipStream_t stream = nullptr;  // copy stream of this slot
+    hipStream_t stream = nullptr;  // this slot's stream (one-tile scratch retries)
     hipEvent_t h2d = nullptr, kdone = nullptr, done = nullptr;
-  } st[2];
+  } st[3];  // triple-buffered: H2D(b+1) and D2H(b-1) overlap kernel(b)
   hipStream_t cstream = nullptr;   // compute stream: kernels serialized (shared scratch)
+  hipStream_t hstream = nullptr;   // every H2D of the host E2E path, in batch order
+  hipStream_t dstream = nullptr;   // every D2H, in batch order (full-duplex PCIe with hstream)
   // diagnostics (TDBG_PROF=1): fused-kernel phase clocks of the last launch
   uint64_t* d_prof = nullptr;
   uint32_t prof_grid = 0;
@@ -430,6 +432,8 @@ void tdbg_context_destroy(tdbg_context* c) {
     if (s.done) (void)hipEventDestroy(s.done);
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->hstream) (void)hipStreamDestroy(c->hstream);
+  if (c->dstream) (void)hipStreamDestroy(c->dstream);
   if (c->d_prof) (void)hipFree(c->d_prof);
   for (auto e : c->tev) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -702,8 +706,30 @@ static int stage_reserve(tdbg_context::Stage& s, uint64_t in_b, uint64_t out_b, 
   return TDBG_OK;
 }
 
-// Coalesced copies: consecutive tiles contiguous in host memory move as one
-// hipMemcpyAsync.
+// Coalesced copies.  Input tiles join the previous tile's copy when they
+// follow it in host memory with at most kInGap bytes of padding between them
+// (e.g. the 16-B alignment a VFS batch read leaves): the padding is copied
+// too, and device offsets keep the host spacing (in_dev_offsets).  Output
+// tiles join only when exactly contiguous: padding must never be overwritten.
+static constexpr uint64_t kInGap = 64;
+
+static bool in_joins(const uint8_t* const* host, const uint64_t* size, uint64_t j) {
+  const uint8_t* end = host[j - 1] + size[j - 1];
+  return host[j] >= end && (uint64_t)(host[j] - end) <= kInGap;
+}
+
+// device offsets (relative to the stage's d_in) of tiles [lo, hi); returns the span
+static uint64_t in_dev_offsets(const uint8_t* const* host, const uint64_t* size, uint64_t lo,
+                               uint64_t hi, uint64_t* off) {
+  uint64_t o = 0;
+  for (uint64_t i = lo; i < hi; i++) {
+    if (i > lo && in_joins(host, size, i)) o += (uint64_t)(host[i] - (host[i - 1] + size[i - 1]));
+    if (off) off[i - lo] = o;
+    o += size[i];
+  }
+  return o;
+}
+
 static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* const* host,
                        const uint64_t* size, uint8_t* dev_base, bool h2d,
                        uint8_t* const* host_out) {
@@ -713,13 +739,15 @@ static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* 
     uint64_t j = i + 1;
     uint64_t bytes = size[i];
     if (h2d) {
-      while (j < hi && host[j] == host[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
+      while (j < hi && in_joins(host, size, j)) { bytes = (uint64_t)(host[j] + size[j] - host[i]); j++; }
       if (bytes) HIP_OK(hipMemcpyAsync(dev_base + doff, host[i], bytes, hipMemcpyHostToDevice, st));
+      doff += bytes;
+      // the next span starts where in_dev_offsets puts it: right after this one
     } else {
       while (j < hi && host_out[j] == host_out[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
       if (bytes) HIP_OK(hipMemcpyAsync(host_out[i], dev_base + doff, bytes, hipMemcpyDeviceToHost, st));
+      doff += bytes;
     }
-    doff += bytes;
     i = j;
   }
   return TDBG_OK;
@@ -736,6 +764,8 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   HIP_OK(hipSetDevice(c->device));
   if (batch_bytes == 0) batch_bytes = 256ull << 20;
   if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  if (!c->hstream) HIP_OK(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  if (!c->dstream) HIP_OK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
   // batches bounded by bytes on both sides
   std::vector<uint64_t> cuts{0};
   uint64_t bi = 0, bo = 0;
@@ -750,8 +780,9 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   cuts.push_back(ntiles);
   std::vector<int32_t> st(ntiles, 0);
   const size_t nb = cuts.size() - 1;
-  std::vector<bool> pending(2, false);
-  std::vector<uint64_t> plo(2), phi(2);
+  constexpr int NS = (int)(sizeof(c->st) / sizeof(c->st[0]));
+  std::vector<bool> pending(NS, false);
+  std::vector<uint64_t> plo(NS), phi(NS);
   auto collect = [&](int k) -> int {
     auto& S = c->st[k];
     HIP_OK(hipEventSynchronize(S.done));
@@ -760,12 +791,15 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     return TDBG_OK;
   };
   for (size_t b = 0; b < nb; b++) {
-    const int k = (int)(b & 1);
+    // slot k is reused once its previous batch's D2H is done (host wait);
+    // the other slots' copies and kernels stay queued meanwhile
+    const int k = (int)(b % NS);
     auto& S = c->st[k];
     if (pending[k]) { int rc = collect(k); if (rc) return rc; }
     const uint64_t lo = cuts[b], hi = cuts[b + 1], nt = hi - lo;
-    uint64_t ib = 0, ob = 0;
-    for (uint64_t i = lo; i < hi; i++) { ib += in_size[i]; ob += out_size[i]; }
+    uint64_t ob = 0;
+    for (uint64_t i = lo; i < hi; i++) ob += out_size[i];
+    const uint64_t ib = in_dev_offsets(in, in_size, lo, hi, nullptr);
     int rc = stage_reserve(S, ib + 16, ob + 16, nt);
     if (rc) return rc;
     // pointer/size arrays (pinned) -> device
@@ -773,23 +807,23 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     uint64_t* hs = (uint64_t*)(hp + nt);
     uint8_t** ho = (uint8_t**)(hs + nt);
     uint64_t* hos = (uint64_t*)(ho + nt);
-    uint64_t io = 0, oo = 0;
+    in_dev_offsets(in, in_size, lo, hi, (uint64_t*)hp);  // offsets first, pointers below
+    uint64_t oo = 0;
     for (uint64_t i = lo; i < hi; i++) {
-      hp[i - lo] = S.d_in + io;
+      hp[i - lo] = S.d_in + (uint64_t)(uintptr_t)hp[i - lo];
       hs[i - lo] = in_size[i];
       ho[i - lo] = S.d_out + oo;
       hos[i - lo] = out_size[i];
-      io += in_size[i];
       oo += out_size[i];
     }
-    HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, S.stream));
-    rc = copy_ranges(S.stream, lo, hi, in, in_size, S.d_in, true, nullptr);
+    HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, c->hstream));
+    rc = copy_ranges(c->hstream, lo, hi, in, in_size, S.d_in, true, nullptr);
     if (rc) return rc;
     const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
     const uint64_t* ds = (const uint64_t*)(dp + nt);
     uint8_t* const* dop = (uint8_t* const*)(ds + nt);
     const uint64_t* dos = (const uint64_t*)(dop + nt);
-    HIP_OK(hipEventRecord(S.h2d, S.stream));
+    HIP_OK(hipEventRecord(S.h2d, c->hstream));
     // kernels serialize on the compute stream (they share the scratch slots)
     HIP_OK(hipStreamWaitEvent(c->cstream, S.h2d, 0));
     rc = ensure_status(c, nt);
@@ -797,16 +831,16 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     rc = launch(c, p, nt, dp, ds, dop, dos, flags, S.d_stat, c->d_need, nullptr, c->cstream, false);
     if (rc) return rc;
     HIP_OK(hipEventRecord(S.kdone, c->cstream));
-    HIP_OK(hipStreamWaitEvent(S.stream, S.kdone, 0));
-    HIP_OK(hipMemcpyAsync(S.h_status, S.d_stat, nt * 4, hipMemcpyDeviceToHost, S.stream));
-    rc = copy_ranges(S.stream, lo, hi, nullptr, out_size, S.d_out, false, out);
+    HIP_OK(hipStreamWaitEvent(c->dstream, S.kdone, 0));
+    HIP_OK(hipMemcpyAsync(S.h_status, S.d_stat, nt * 4, hipMemcpyDeviceToHost, c->dstream));
+    rc = copy_ranges(c->dstream, lo, hi, nullptr, out_size, S.d_out, false, out);
     if (rc) return rc;
-    HIP_OK(hipEventRecord(S.done, S.stream));
+    HIP_OK(hipEventRecord(S.done, c->dstream));
     pending[k] = true;
     plo[k] = lo;
     phi[k] = hi;
   }
-  for (int k = 0; k < 2; k++)
+  for (int k = 0; k < NS; k++)
     if (pending[k]) { int rc = collect(k); if (rc) return rc; }
   c->tiles_unfiltered += ntiles;
   // tiles that needed bigger scratch: redo them one by one through the sync path
