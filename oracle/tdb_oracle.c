@@ -126,7 +126,33 @@ static uint8_t output_datatype(const oracle_filter* f, uint8_t in) {
   if ((f->type == TDBG_FILTER_DOUBLE_DELTA || f->type == TDBG_FILTER_DELTA) &&
       f->reinterpret != TDBG_ANY)
     return f->reinterpret;
+  /* XORFilter::output_datatype xor_filter.cc:63-78: the signed integer of
+   * the input's width (other widths throw; kept as is, the filter fails) */
+  if (f->type == TDBG_FILTER_XOR) {
+    switch (oracle_datatype_size(in)) {
+      case 1: return TDBG_INT8;
+      case 2: return TDBG_INT16;
+      case 4: return TDBG_INT32;
+      case 8: return TDBG_INT64;
+      default: return in;
+    }
+  }
   return in;
+}
+
+/* XORFilter::xor_part / unxor_part (xor_filter.cc:149-177, 260-286):
+ * out[0] = in[0]; forward out[j] = in[j] ^ in[j-1], reverse
+ * out[j] = in[j] ^ out[j-1], over the part's n/ts whole elements.  The
+ * reference writes nothing for a part's n % ts tail bytes (its forward output
+ * holds whatever the fresh buffer held); here the forward zero-fills them and
+ * the reverse leaves them untouched, so tails are parity-unpinned. */
+static void xor_part(int inverse, uint32_t ts, const uint8_t* in, uint64_t n, uint8_t* out) {
+  uint64_t ne = n / ts, prev = 0;
+  for (uint64_t j = 0; j < ne; j++) {
+    uint64_t v = ld(in + j * ts, ts), o = j == 0 ? v : v ^ prev;
+    st(out + j * ts, o, ts);
+    prev = inverse ? o : v;
+  }
 }
 
 static int is_compression_type(uint8_t t) {
@@ -646,6 +672,23 @@ static int fwd_filter(const oracle_pipeline* p, const oracle_filter* f,
       plist_push(D2, out, dsize);
       return md_prepend(M2, hdr, 4 + 4 * (uint64_t)D->np, M);
     }
+    case TDBG_FILTER_XOR: { /* xor_filter.cc:120-146: one part per input buffer */
+      uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype);
+      if (ts != 1 && ts != 2 && ts != 4 && ts != 8) return TDBG_E_ARG;
+      uint8_t* out = arena_alloc(ar, dsize);
+      uint8_t* hdr = arena_alloc(ar, 4 + 4 * (uint64_t)D->np);
+      if (!out || !hdr) return TDBG_E_ARG;
+      memset(out, 0, dsize);
+      st(hdr, (uint64_t)D->np, 4);
+      uint64_t o = 0;
+      for (int i = 0; i < D->np; i++) {
+        st(hdr + 4 + 4 * i, D->v[i].n, 4);
+        xor_part(0, ts, D->v[i].p, D->v[i].n, out + o);
+        o += D->v[i].n;
+      }
+      plist_push(D2, out, dsize);
+      return md_prepend(M2, hdr, 4 + 4 * (uint64_t)D->np, M);
+    }
     case TDBG_FILTER_BITSHUFFLE: { /* bitshuffle_filter.cc:63-126 */
       uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype);
       plist_t parts = {0};
@@ -1046,9 +1089,13 @@ static int rev_filter(const oracle_pipeline* p, const oracle_filter* f,
     case TDBG_FILTER_NONE:
       PASS_THROUGH();
     case TDBG_FILTER_BYTESHUFFLE:
-    case TDBG_FILTER_BITSHUFFLE: {
-      /* byteshuffle_filter.cc:111-147, bitshuffle_filter.cc:168-212 */
+    case TDBG_FILTER_BITSHUFFLE:
+    case TDBG_FILTER_XOR: {
+      /* byteshuffle_filter.cc:111-147, bitshuffle_filter.cc:168-212,
+       * xor_filter.cc:220-256 (same md / part walk) */
       uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype);
+      if (f->type == TDBG_FILTER_XOR && ts != 1 && ts != 2 && ts != 4 && ts != 8)
+        return TDBG_E_UNSUPPORTED; /* "datatype size cannot be converted" */
       uint32_t np;
       if ((rc = md_read(md, &np, 4))) return rc;
       if ((rc = out_prepend(out, in_n))) return rc;
@@ -1059,6 +1106,8 @@ static int rev_filter(const oracle_pipeline* p, const oracle_filter* f,
         if (ip + ps > in_n) return TDBG_E_DATA_READ; /* get_const_buffer */
         if (f->type == TDBG_FILTER_BYTESHUFFLE)
           oracle_byteshuffle(1, ts, in + ip, ps, out->p + ip);
+        else if (f->type == TDBG_FILTER_XOR)
+          xor_part(1, ts, in + ip, ps, out->p + ip);
         else if (ps % ts != 0 || ps % 8 != 0)
           memcpy(out->p + ip, in + ip, ps);
         else

@@ -16,7 +16,7 @@ import numpy as np
 from tiledb_amd.filter_pipeline import (FORMAT_VERSION, BitshuffleFilter, BitWidthReductionFilter,
                                         ByteshuffleFilter, CompressionFilter, Compressor, Datatype,
                                         FilterPipeline, NoopFilter, PositiveDeltaFilter,
-                                        datatype_size)
+                                        XORFilter, datatype_size)
 
 
 @dataclass
@@ -280,6 +280,23 @@ def edge_cases() -> List[Case]:
     cases.append(Case("incomp_c5_mixed_raw_and_packed", c5p, I32, 4, mixed))
     cases.append(Case("incomp_c5_offsets_u64", c5p, U64, 8,
                       [rng.integers(0, 256, 8 * 8191, dtype=np.uint8)], offsets_tile=True))
+    # XOR (xor_filter.cc): every width, float inputs whose
+    # XOR output type (INT32/INT64) makes a following BWR / DD active,
+    # multi-chunk tiles, XOR after a shuffle (md stack)
+    for dt in (Datatype.INT8, Datatype.UINT16, Datatype.INT32, Datatype.UINT64):
+        sz = datatype_size(dt)
+        v = np.cumsum(rng.integers(0, 50, 4000)).astype(np.int64).astype(
+            {1: np.uint8, 2: np.uint16, 4: np.int32, 8: np.uint64}[sz])
+        cases.append(Case(f"xor_{dt.name}", P(XORFilter()), dt, sz, [as_u8(v)]))
+    f32 = (1000 * np.sin(np.arange(16384) * 1e-3)).astype(np.float32)
+    cases.append(Case("xor_f32_then_bwr", P(XORFilter(), BitWidthReductionFilter(256)),
+                      Datatype.FLOAT32, 4, [as_u8(f32)]))
+    f64 = 1.0 + np.cumsum(rng.integers(0, 9, 8192)) * 2.0 ** -30  # one exponent: small XORs
+    cases.append(Case("xor_f64_then_dd", P(XORFilter(), DD()), Datatype.FLOAT64, 8, [as_u8(f64)]))
+    cases.append(Case("xor_multichunk_i32", P(XORFilter(), BitshuffleFilter()), I32, 4,
+                      [as_u8(np.arange(30000, dtype=np.int32) * 3)], max_chunk=4096))
+    cases.append(Case("byteshuffle_then_xor_i64", P(ByteshuffleFilter(), XORFilter()), I64, 8,
+                      [as_u8(np.arange(7000, dtype=np.int64) ** 2)]))
     return cases
 
 

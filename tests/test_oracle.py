@@ -349,3 +349,32 @@ def test_numpy_config_encoders_match_oracle(oracle_mod, name):
             assert f == op.filter_tile(v), f"{name} {variant} tile {k}"
             rc, out = op.unfilter_tile(f, v.nbytes)
             assert rc == 0 and np.array_equal(out, v.view(np.uint8))
+
+
+def test_xor_known_answer_and_type_chain(oracle_mod):
+    """XOR forward = x[j] ^ x[j-1] with x[0] kept (xor_filter.cc:149-177), its
+    reverse the prefix XOR (:260-286); the output type is the signed integer of
+    the input width (:63-78), so BWR after XOR on FLOAT32 is active."""
+    from tiledb_amd.filter_pipeline import XORFilter, BitWidthReductionFilter
+    x = np.array([5, 3, 3, 8, -1, 0x7FFFFFFF], dtype=np.int32)
+    op = oracle_mod.OraclePipeline(P(XORFilter()).serialize(), 23, int(Datatype.INT32), 4)
+    f = np.frombuffer(op.filter_tile(as_u8(x)), dtype=np.uint8)
+    # tile header 8 + chunk header 12 + md [u32 nparts=1][u32 24] + data
+    assert int(f[16:20].view(np.uint32)[0]) == 8
+    assert f[20:28].view(np.uint32).tolist() == [1, 24]
+    want = x.copy()
+    want[1:] = x[1:] ^ x[:-1]
+    assert np.array_equal(f[28:].view(np.int32), want)
+    rc, back = op.unfilter_tile(f, x.nbytes)
+    assert rc == 0 and np.array_equal(back.view(np.int32), x)
+    # FLOAT32 -> XOR -> INT32: the BWR md then holds window entries
+    v = (np.arange(1024) * 0.5).astype(np.float32)
+    ser = P(XORFilter(), BitWidthReductionFilter(256)).serialize()
+    fp = FilterPipeline.deserialize(ser, 23, Datatype.FLOAT32)
+    assert fp.filters[1].filter_data_type == Datatype.INT32
+    op2 = oracle_mod.OraclePipeline(ser, 23, int(Datatype.FLOAT32), 4)
+    f2 = np.frombuffer(op2.filter_tile(as_u8(v)), dtype=np.uint8)
+    md_len = int(f2[16:20].view(np.uint32)[0])
+    assert md_len == 8 + 16 * 9 + 8  # BWR: orig, nwin, 16 x (i32, u8, u32); XOR: nparts, size
+    rc, back = op2.unfilter_tile(f2, v.nbytes)
+    assert rc == 0 and np.array_equal(back.view(np.float32), v)

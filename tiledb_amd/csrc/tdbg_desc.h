@@ -19,7 +19,8 @@ enum tdbg_stage_kind : uint8_t {
   TDBG_K_PD = 4,          // PositiveDeltaFilter::run_reverse<T>
   TDBG_K_DD = 5,          // CompressionFilter + DoubleDelta::decompress<T>
   TDBG_K_RLE = 6,         // CompressionFilter + RLE::decompress
-  TDBG_K_UNSUPPORTED = 7
+  TDBG_K_XOR = 7,         // XORFilter::run_reverse<T> (prefix XOR; general interpreter only)
+  TDBG_K_UNSUPPORTED = 8
 };
 
 struct tdbg_stage {

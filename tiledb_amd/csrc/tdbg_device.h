@@ -69,6 +69,30 @@ __device__ __forceinline__ uint64_t wave_incscan_u64(uint64_t x) {
   return x;
 }
 
+// Inclusive prefix XOR of one u64 per thread over the workgroup (XOR
+// filter); total = XOR of all; red >= NT/64 entries of LDS.
+template <int NT = GEN_NT>
+__device__ __forceinline__ uint64_t block_incscan_xor(uint64_t x, uint64_t& total, uint64_t* red) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x ^= y;
+  }
+  if (lane == 63) red[wid] = x;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const uint64_t s = red[i];
+    if ((uint32_t)i < wid) pre ^= s;
+    tot ^= s;
+  }
+  __syncthreads();
+  total = tot;
+  return pre ^ x;
+}
+
 // Exclusive block scan of one u64 per thread; red >= NT/64 entries of LDS.
 template <int NT = GEN_NT>
 __device__ __forceinline__ uint64_t block_exscan_u64(uint64_t v, uint64_t& total,

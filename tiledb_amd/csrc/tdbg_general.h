@@ -92,6 +92,27 @@ __device__ void g_bitunshuffle_part(uint8_t* dst, const uint8_t* src,
 }
 
 // ---------------------------------------------------------------------------
+// XOR^-1 of one part (XORFilter::unxor_part, xor_filter.cc:260-286):
+// out[j] = in[0] ^ ... ^ in[j] over the part's n/ts whole elements, one
+// block prefix-XOR per NT elements with a running carry.  The n % ts tail
+// bytes are not written (the reference does not write them either).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ void g_unxor_part(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t ts,
+                             Shared<NT>& sh) {
+  const uint64_t ne = n / ts;
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < ne; b += NT) {
+    const uint64_t j = b + threadIdx.x;
+    const uint64_t v = j < ne ? ldn(src + j * ts, ts) : 0;
+    uint64_t tot;
+    const uint64_t x = block_incscan_xor<NT>(v, tot, sh.red) ^ carry;
+    if (j < ne) stn(dst + j * ts, x, ts);
+    carry ^= tot;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // BWR^-1 (bit_width_reduction_filter.cc:352-404)
 // md: [u32 orig][u32 nwin] nwin x [T offset][u8 bits][u32 nbytes]
 // ---------------------------------------------------------------------------
@@ -486,7 +507,8 @@ __device__ __attribute__((noinline)) int g_chunk(const tdbg_plan& P, const uint8
         }
         break;
       case TDBG_K_BYTESHUFFLE:
-      case TDBG_K_BITSHUFFLE: {
+      case TDBG_K_BITSHUFFLE:
+      case TDBG_K_XOR: {  // same md / part walk (xor_filter.cc:220-256)
         if (md_n < 4) { rc = TDBG_E_MD_READ; break; }
         const uint32_t np = (uint32_t)ldn(mdp, 4);
         if (io.fixed) { if (cin_n > io.cap) { rc = TDBG_E_OUT_FULL; break; } }
@@ -497,6 +519,7 @@ __device__ __attribute__((noinline)) int g_chunk(const tdbg_plan& P, const uint8
           const uint32_t ps = (uint32_t)ldn(mdp + 4 + 4 * i, 4);
           if (ip + ps > cin_n) { rc = TDBG_E_DATA_READ; break; }
           if (s.kind == TDBG_K_BYTESHUFFLE) g_unshuffle_part<NT>(io.out + ip, cin + ip, ps, s.w);
+          else if (s.kind == TDBG_K_XOR) g_unxor_part<NT>(io.out + ip, cin + ip, ps, s.w, sh);
           else g_bitunshuffle_part<NT>(io.out + ip, cin + ip, ps, s.w);
           ip += ps;
         }

@@ -209,6 +209,17 @@ void build_plan(tdbg_pipeline* p) {
         s.kind = TDBG_K_BITSHUFFLE;
         s.w = (uint8_t)dt_size(dt);
         break;
+      case TDBG_FILTER_XOR: {  // xor_filter.cc:179-218: integer of the type's width
+        const uint64_t w = dt_size(dt);
+        if (w == 1 || w == 2 || w == 4 || w == 8) {
+          s.kind = TDBG_K_XOR;
+          s.w = (uint8_t)w;
+        } else {
+          s.kind = TDBG_K_UNSUPPORTED;
+          p->supported = false;
+        }
+        break;
+      }
       case TDBG_FILTER_BIT_WIDTH_REDUCTION:
       case TDBG_FILTER_POSITIVE_DELTA: {
         const bool bwr = f.type == TDBG_FILTER_BIT_WIDTH_REDUCTION;
@@ -374,6 +385,15 @@ int tdbg_pipeline_create(const uint8_t* b, size_t len, uint32_t version,
     if ((f.type == TDBG_FILTER_DOUBLE_DELTA || f.type == TDBG_FILTER_DELTA) &&
         f.reinterpret != TDBG_ANY)
       cur = f.reinterpret;  // CompressionFilter::output_datatype
+    if (f.type == TDBG_FILTER_XOR) {  // XORFilter::output_datatype xor_filter.cc:63-78
+      switch (dt_size(cur)) {
+        case 1: cur = TDBG_INT8; break;
+        case 2: cur = TDBG_INT16; break;
+        case 4: cur = TDBG_INT32; break;
+        case 8: cur = TDBG_INT64; break;
+        default: break;  // the reference throws; build_plan marks it unsupported
+      }
+    }
     p->filters.push_back(f);
   }
   build_plan(p);

@@ -252,6 +252,24 @@ class PositiveDeltaFilter(Filter):
         return f"PositiveDelta: POSITIVE_DELTA_MAX_WINDOW={self.max_window_size}"
 
 
+class XORFilter(Filter):
+    """xor_filter.cc: prefix XOR of the input's integer width, any 1/2/4/8-byte
+    type (:51-61); output type = the signed integer of that width (:63-78)."""
+
+    type = FilterType.FILTER_XOR
+
+    def accepts_input_datatype(self, datatype: int) -> bool:
+        return datatype_size(datatype) in (1, 2, 4, 8)
+
+    def output_datatype(self, input_type: int) -> Datatype:
+        w = datatype_size(input_type)
+        m = {1: Datatype.INT8, 2: Datatype.INT16, 4: Datatype.INT32, 8: Datatype.INT64}
+        if w not in m:
+            raise FilterStatusException(
+                "XORFilter::output_datatype: datatype size cannot be converted to integer type.")
+        return m[w]
+
+
 class CompressionFilter(Filter):
     """compression_filter.cc.  The filter type follows the compressor."""
 
@@ -391,6 +409,8 @@ class FilterPipeline:
                 f = BitshuffleFilter(dt)
             elif ftype == FilterType.FILTER_BYTESHUFFLE:
                 f = ByteshuffleFilter(dt)
+            elif ftype == FilterType.FILTER_XOR:
+                f = XORFilter(dt)
             else:
                 o += mdlen
                 f = Filter(dt)

@@ -11,10 +11,11 @@ import workloads as W
 from tiledb_amd import engine
 
 NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c", "final", "tail", "-"]
-dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+_ser, _dt, _cs, _, _ = W.config("c5")
+dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)
 for var in sys.argv[1:] or ["rand", "ramp"]:
-    batch = bench.build_batch(engine, var, 12500, 128, 0, seed=5)[0]
+    batch = bench.build_batch(engine, "c5", var, 12500, 128, 0, seed=5)[0]
     for _ in range(3):
         ctx.unfilter_async(dp, batch)
     torch.cuda.synchronize()
