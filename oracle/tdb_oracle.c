@@ -603,6 +603,50 @@ int oracle_dd_decompress(uint8_t dtype, const uint8_t* in, uint64_t n,
   return dd_decompress_w(dtype, in, n, out, out_size, &w);
 }
 
+/* Delta::compress / decompress (delta_compressor.cc:224-249, 251-273); the
+ * value type table is DoubleDelta's (dd_type; delta_compressor.cc:60-217).
+ * Forward: [u64 num][T x0][T (x[i] - x[i-1])]..., the difference truncated
+ * to T (wrapping).  Reverse: x[i] = (T)(x[i-1] + d[i]); x0 is read and
+ * written even when num == 0.  Reads fail before the write at the same index
+ * (DATA_READ), writes past the part's size fail with OUT_FULL.  Bytes past
+ * the decoded values are unspecified in the reference; zero here. */
+static int delta_compress(uint8_t dtype, const uint8_t* in, uint64_t n,
+                          uint8_t* out, uint64_t cap, uint64_t* out_n) {
+  ival_t t;
+  int rc = dd_type(dtype, &t);
+  if (rc) return rc;
+  uint64_t num = n / t.w;
+  if (cap < 8 + (num ? num : 1) * t.w) return TDBG_E_ARG;
+  memcpy(out, &num, 8);
+  st(out + 8, num ? ld(in, t.w) : 0, t.w);
+  for (uint64_t i = 1; i < num; i++)
+    st(out + 8 + i * t.w, (ld(in + i * t.w, t.w) - ld(in + (i - 1) * t.w, t.w)) & mask_w(t.w), t.w);
+  *out_n = 8 + (num ? num : 1) * t.w;
+  return TDBG_OK;
+}
+
+static int delta_decompress_w(uint8_t dtype, const uint8_t* in, uint64_t n,
+                              uint8_t* out, uint64_t out_size, uint64_t* written) {
+  ival_t t;
+  *written = 0;
+  int rc = dd_type(dtype, &t);
+  if (rc) return rc;
+  uint64_t num = 0;
+  if (n < 8) return TDBG_E_DATA_READ;
+  memcpy(&num, in, 8);
+  uint64_t nv = num ? num : 1, prev = 0;
+  for (uint64_t i = 0; i < nv; i++) {
+    if (8 + (i + 1) * t.w > n) return TDBG_E_DATA_READ;
+    if ((i + 1) * t.w > out_size) return TDBG_E_OUT_FULL;
+    uint64_t d = ld(in + 8 + i * t.w, t.w);
+    prev = i == 0 ? d : (prev + d) & mask_w(t.w);
+    st(out + i * t.w, prev, t.w);
+    *written = (i + 1) * t.w;
+  }
+  if (*written < out_size) memset(out + *written, 0, out_size - *written);
+  return TDBG_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Forward pipeline (fixture producer)                                       */
 /* ------------------------------------------------------------------------ */
@@ -872,6 +916,7 @@ static int fwd_filter(const oracle_pipeline* p, const oracle_filter* f,
       return md_prepend(M2, hdr, mdn, M);
     }
     case TDBG_FILTER_RLE:
+    case TDBG_FILTER_DELTA:
     case TDBG_FILTER_DOUBLE_DELTA: { /* compression_filter.cc:240-301 */
       plist_t parts = {0};
       for (int i = 0; i < M->np; i++) plist_push(&parts, M->v[i].p, M->v[i].n);
@@ -893,6 +938,8 @@ static int fwd_filter(const oracle_pipeline* p, const oracle_filter* f,
         uint64_t cl = 0;
         if (f->type == TDBG_FILTER_RLE)
           rc = oracle_rle_compress(p->cell_size, parts.v[i].p, parts.v[i].n, out + o, ub + 64 - o, &cl);
+        else if (f->type == TDBG_FILTER_DELTA)
+          rc = delta_compress(ddt, parts.v[i].p, parts.v[i].n, out + o, ub + 64 - o, &cl);
         else
           rc = oracle_dd_compress(ddt, parts.v[i].p, parts.v[i].n, out + o, ub + 64 - o, &cl);
         if (rc) return rc;
@@ -1190,6 +1237,7 @@ static int rev_filter(const oracle_pipeline* p, const oracle_filter* f,
       return TDBG_OK;
     }
     case TDBG_FILTER_RLE:
+    case TDBG_FILTER_DELTA:
     case TDBG_FILTER_DOUBLE_DELTA: {
       if (f->compressor == TDBG_COMPRESSOR_NONE) PASS_THROUGH();
       /* compression_filter.cc:303-347, 413-486 */
@@ -1224,6 +1272,8 @@ static int rev_filter(const oracle_pipeline* p, const oracle_filter* f,
         uint64_t wr;
         if (f->type == TDBG_FILTER_RLE)
           rc = rle_decompress_w(p->cell_size, in + ip, cn, dst, un, &wr);
+        else if (f->type == TDBG_FILTER_DELTA)
+          rc = delta_decompress_w(ddt, in + ip, cn, dst, un, &wr);
         else
           rc = dd_decompress_w(ddt, in + ip, cn, dst, un, &wr);
         if (rc) goto fail;

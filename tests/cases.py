@@ -49,6 +49,10 @@ def RLE():
     return CompressionFilter(Compressor.RLE, -1)
 
 
+def DELTA(reinterpret=Datatype.ANY):
+    return CompressionFilter(Compressor.DELTA, -1, reinterpret_datatype=reinterpret)
+
+
 def as_u8(a: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(a).view(np.uint8).reshape(-1)
 
@@ -297,6 +301,22 @@ def edge_cases() -> List[Case]:
                       [as_u8(np.arange(30000, dtype=np.int32) * 3)], max_chunk=4096))
     cases.append(Case("byteshuffle_then_xor_i64", P(ByteshuffleFilter(), XORFilter()), I64, 8,
                       [as_u8(np.arange(7000, dtype=np.int64) ** 2)]))
+    # DELTA compressor (delta_compressor.cc): widths, wrapping
+    # differences, reinterpret, md parts (shuffle md through the frame), multi-chunk
+    cases.append(Case("delta_i32", P(DELTA()), I32, 4,
+                      [as_u8(np.cumsum(rng.integers(-1000, 1000, 16384)).astype(np.int32))]))
+    cases.append(Case("delta_u8_wrap", P(DELTA()), Datatype.UINT8, 1,
+                      [rng.integers(0, 256, 5000, dtype=np.uint8)]))
+    cases.append(Case("delta_u64_extremes", P(DELTA()), U64, 8,
+                      [as_u8(np.array([0, 2**64 - 1, 1, 2**63, 5] * 300, dtype=np.uint64))]))
+    cases.append(Case("delta_i16_one_value", P(DELTA()), Datatype.INT16, 2,
+                      [as_u8(np.array([-7], dtype=np.int16))]))
+    cases.append(Case("delta_reinterpret_u8_as_i32", P(DELTA(Datatype.INT32)), Datatype.UINT8, 1,
+                      [as_u8(np.arange(4000, dtype=np.int32) * 3)]))
+    cases.append(Case("byteshuffle_delta_bwr", P(ByteshuffleFilter(), DELTA(), BitWidthReductionFilter(256)),
+                      I32, 4, [as_u8(np.arange(16384, dtype=np.int32) * 5)]))
+    cases.append(Case("delta_multichunk_i64", P(DELTA()), I64, 8,
+                      [as_u8(np.cumsum(rng.integers(0, 9, 30000)).astype(np.int64))], max_chunk=8192))
     return cases
 
 

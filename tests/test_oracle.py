@@ -378,3 +378,23 @@ def test_xor_known_answer_and_type_chain(oracle_mod):
     assert md_len == 8 + 16 * 9 + 8  # BWR: orig, nwin, 16 x (i32, u8, u32); XOR: nparts, size
     rc, back = op2.unfilter_tile(f2, v.nbytes)
     assert rc == 0 and np.array_equal(back.view(np.float32), v)
+
+
+def test_delta_known_answer(oracle_mod):
+    """DELTA part = [u64 num][T x0][T x[i]-x[i-1]...] (delta_compressor.cc:224-249) in the
+    compression frame [u32 n_md][u32 n_data][u32 orig][u32 comp] (compression_filter.cc:240-301)."""
+    from tests.cases import DELTA
+    x = np.array([10, 7, 7, 20], dtype=np.int32)
+    op = oracle_mod.OraclePipeline(P(DELTA()).serialize(), 23, int(Datatype.INT32), 4)
+    f = np.frombuffer(op.filter_tile(as_u8(x)), dtype=np.uint8)
+    assert int(f[16:20].view(np.uint32)[0]) == 16
+    assert f[20:36].view(np.uint32).tolist() == [0, 1, 16, 24]
+    assert int(f[36:44].view(np.uint64)[0]) == 4
+    assert f[44:60].view(np.int32).tolist() == [10, -3, 0, 13]
+    rc, back = op.unfilter_tile(f, x.nbytes)
+    assert rc == 0 and np.array_equal(back.view(np.int32), x)
+    # num claims more values than the part holds: the read fails first
+    g = f.copy()
+    g[36] = 5
+    rc, _ = op.unfilter_tile(g, x.nbytes)
+    assert rc == 5  # TDBG_E_DATA_READ

@@ -20,7 +20,8 @@ enum tdbg_stage_kind : uint8_t {
   TDBG_K_DD = 5,          // CompressionFilter + DoubleDelta::decompress<T>
   TDBG_K_RLE = 6,         // CompressionFilter + RLE::decompress
   TDBG_K_XOR = 7,         // XORFilter::run_reverse<T> (prefix XOR; general interpreter only)
-  TDBG_K_UNSUPPORTED = 8
+  TDBG_K_DELTA = 8,       // CompressionFilter + Delta::decompress<T> (general interpreter only)
+  TDBG_K_UNSUPPORTED = 9
 };
 
 struct tdbg_stage {

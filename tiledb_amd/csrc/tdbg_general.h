@@ -414,6 +414,37 @@ __device__ int g_rle_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
 }
 
 // ---------------------------------------------------------------------------
+// Delta::decompress<T> of one part (delta_compressor.cc:251-273):
+// [u64 num][T x0][T d1..], x[i] = (T)(x[i-1] + d[i]), x0 written even when
+// num == 0.  Status as the reference's first failing call: the read of value
+// i (DATA_READ) comes before its write (OUT_FULL).  One block scan per NT
+// values with a running carry; bytes past the values are zeroed (unspecified
+// in the reference, zeroed by the oracle too).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ int g_delta_part(const uint8_t* src, uint64_t cn, uint8_t* dst, uint64_t un,
+                            uint32_t w, Shared<NT>& sh) {
+  if (w == 0) return TDBG_E_DD_TYPE;
+  if (cn < 8) return TDBG_E_DATA_READ;
+  const uint64_t num = ldn(src, 8);
+  const uint64_t nv = num ? num : 1;
+  const uint64_t kr = (cn - 8) / w, kw = un / w;  // values readable / writable
+  if (nv > kr || nv > kw) return kr <= kw ? TDBG_E_DATA_READ : TDBG_E_OUT_FULL;
+  const uint64_t m = wmask(w);
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < nv; b += NT) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t d = i < nv ? ldn(src + 8 + i * w, w) : 0;
+    uint64_t tot;
+    const uint64_t x = carry + block_exscan_u64<NT>(d, tot, sh.red) + d;
+    if (i < nv) stn(dst + i * w, x & m, w);
+    carry += tot;
+  }
+  if (nv * w < un) g_zero<NT>(dst + nv * w, un - nv * w);
+  return TDBG_OK;
+}
+
+// ---------------------------------------------------------------------------
 // CompressionFilter::run_reverse (compression_filter.cc:303-347) for DD/RLE
 // md: [u32 n_md][u32 n_data] (u32 orig, u32 comp) x (n_md + n_data)
 // ---------------------------------------------------------------------------
@@ -451,6 +482,7 @@ __device__ int g_compression(StageIO& io, const tdbg_stage& s, Slot& sl,
     if (ip + cn > io.in_n) return TDBG_E_DATA_READ;
     int rc;
     if (s.kind == TDBG_K_DD) rc = g_dd_part<NT>(io.in + ip, cn, dst, un, s.w, sh);
+    else if (s.kind == TDBG_K_DELTA) rc = g_delta_part<NT>(io.in + ip, cn, dst, un, s.w, sh);
     else rc = g_rle_part<NT>(io.in + ip, cn, dst, un, s.cs, sl, sh, &io.need);
     __syncthreads();
     if (rc) return rc;
@@ -534,6 +566,7 @@ __device__ __attribute__((noinline)) int g_chunk(const tdbg_plan& P, const uint8
         rc = g_pd<NT>(io, s, sl, sh);
         break;
       case TDBG_K_DD:
+      case TDBG_K_DELTA:
       case TDBG_K_RLE: {
         const int md_dst = md_buf == 0 ? 1 : 0;
         uint64_t mo = 0;
@@ -555,7 +588,8 @@ __device__ __attribute__((noinline)) int g_chunk(const tdbg_plan& P, const uint8
       if (rc == TDBG_E_SCRATCH) *need = io.need;
       return rc;
     }
-    if (s.kind != TDBG_K_DD && s.kind != TDBG_K_RLE && s.kind != TDBG_K_PASS) {
+    if (s.kind != TDBG_K_DD && s.kind != TDBG_K_DELTA && s.kind != TDBG_K_RLE &&
+        s.kind != TDBG_K_PASS) {
       mdp += io.md_used;
       md_n -= io.md_used;
     }

@@ -257,8 +257,10 @@ void build_plan(tdbg_pipeline* p) {
           s.kind = TDBG_K_RLE;
           s.cs = p->cell_size;
           if (p->cell_size == 0) { s.kind = TDBG_K_UNSUPPORTED; p->supported = false; }
-        } else if (f.compressor == TDBG_COMPRESSOR_DOUBLE_DELTA) {
-          s.kind = TDBG_K_DD;
+        } else if (f.compressor == TDBG_COMPRESSOR_DOUBLE_DELTA ||
+                   f.compressor == TDBG_COMPRESSOR_DELTA) {
+          // Delta::decompress (delta_compressor.cc:139-217) uses DoubleDelta's type table
+          s.kind = f.compressor == TDBG_COMPRESSOR_DELTA ? TDBG_K_DELTA : TDBG_K_DD;
           const uint8_t t = f.reinterpret != TDBG_ANY ? f.reinterpret : dt;
           switch (t) {
             case TDBG_FLOAT32: case TDBG_FLOAT64: s.w = 0; break;  // DD_TYPE at run time
