@@ -30,7 +30,7 @@ class OraclePipelineStruct(ctypes.Structure):
         ("version", ctypes.c_uint32),
         ("on_disk_type", ctypes.c_uint8),
         ("cell_size", ctypes.c_uint64),
-        ("f", (ctypes.c_uint8 * 20) * 32),  # opaque: oracle_filter[32]
+        ("f", (ctypes.c_uint64 * 8) * 32),  # opaque, >= sizeof(oracle_filter)[32]
     ]
 
 

@@ -15,6 +15,7 @@
  */
 #include "tdb_oracle.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -128,6 +129,16 @@ static uint8_t output_datatype(const oracle_filter* f, uint8_t in) {
     return f->reinterpret;
   /* XORFilter::output_datatype xor_filter.cc:63-78: the signed integer of
    * the input's width (other widths throw; kept as is, the filter fails) */
+  /* FloatScalingFilter::output_datatype float_scaling_filter.cc:313-327 */
+  if (f->type == TDBG_FILTER_SCALE_FLOAT) {
+    switch (f->byte_width) {
+      case 1: return TDBG_INT8;
+      case 2: return TDBG_INT16;
+      case 4: return TDBG_INT32;
+      case 8: return TDBG_INT64;
+      default: return in;
+    }
+  }
   if (f->type == TDBG_FILTER_XOR) {
     switch (oracle_datatype_size(in)) {
       case 1: return TDBG_INT8;
@@ -152,6 +163,42 @@ static void xor_part(int inverse, uint32_t ts, const uint8_t* in, uint64_t n, ui
     uint64_t v = ld(in + j * ts, ts), o = j == 0 ? v : v ^ prev;
     st(out + j * ts, o, ts);
     prev = inverse ? o : v;
+  }
+}
+
+/* FloatScalingFilter forward (float_scaling_filter.cc:60-99): W(round((x -
+ * (T)offset) / (T)scale)) in T arithmetic; reverse (:164-197):
+ * (T)(scale * (double)(T)w + offset), double multiply and add, not fused. */
+static void fscale_fwd(uint32_t ts, uint32_t bw, double sc, double of, const uint8_t* in,
+                       uint64_t ne, uint8_t* out) {
+  for (uint64_t j = 0; j < ne; j++) {
+    int64_t q;
+    if (ts == 4) {
+      float x;
+      memcpy(&x, in + 4 * j, 4);
+      q = (int64_t)roundf((x - (float)of) / (float)sc);
+    } else {
+      double x;
+      memcpy(&x, in + 8 * j, 8);
+      q = (int64_t)round((x - of) / sc);
+    }
+    st(out + bw * j, (uint64_t)q, bw);
+  }
+}
+
+static void fscale_rev(uint32_t ts, uint32_t bw, double sc, double of, const uint8_t* in,
+                       uint64_t ne, uint8_t* out) {
+  for (uint64_t j = 0; j < ne; j++) {
+    int64_t q = sext(ld(in + bw * j, bw), bw);
+    if (ts == 4) {
+      volatile double prod = sc * (double)(float)q;
+      float y = (float)(prod + of);
+      memcpy(out + 4 * j, &y, 4);
+    } else {
+      volatile double prod = sc * (double)q;
+      double y = prod + of;
+      memcpy(out + 8 * j, &y, 8);
+    }
   }
 }
 
@@ -236,8 +283,11 @@ int oracle_pipeline_parse(const uint8_t* b, size_t len, uint32_t version,
       case TDBG_FILTER_AES_256_GCM: case TDBG_FILTER_CHECKSUM_MD5:
       case TDBG_FILTER_CHECKSUM_SHA256: case TDBG_FILTER_XOR:
         break;
-      case TDBG_FILTER_SCALE_FLOAT:
+      case TDBG_FILTER_SCALE_FLOAT: /* FilterConfig {double scale, offset; u64 byte_width} */
         NEED(24);
+        memcpy(&f->scale, b + o, 8);
+        memcpy(&f->offset, b + o + 8, 8);
+        memcpy(&f->byte_width, b + o + 16, 8);
         o += 24;
         break;
       case TDBG_FILTER_WEBP:
@@ -281,6 +331,15 @@ int oracle_pipeline_serialize(const oracle_pipeline* p, uint8_t* out,
                f->type == TDBG_FILTER_CHECKSUM_SHA256) {
       PUT(f->type, 1);
       PUT(0, 4);
+    } else if (f->type == TDBG_FILTER_SCALE_FLOAT) {
+      uint64_t sb, ob;
+      memcpy(&sb, &f->scale, 8);
+      memcpy(&ob, &f->offset, 8);
+      PUT(f->type, 1);
+      PUT(24, 4);
+      PUT(sb, 8);
+      PUT(ob, 8);
+      PUT(f->byte_width, 8);
     } else {
       return TDBG_E_UNSUPPORTED;
     }
@@ -716,6 +775,25 @@ static int fwd_filter(const oracle_pipeline* p, const oracle_filter* f,
       plist_push(D2, out, dsize);
       return md_prepend(M2, hdr, 4 + 4 * (uint64_t)D->np, M);
     }
+    case TDBG_FILTER_SCALE_FLOAT: { /* float_scaling_filter.cc:60-99 */
+      uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype), bw = (uint32_t)f->byte_width;
+      if ((ts != 4 && ts != 8) || (bw != 1 && bw != 2 && bw != 4 && bw != 8)) return TDBG_E_ARG;
+      uint64_t tot = 0;
+      for (int i = 0; i < D->np; i++) tot += D->v[i].n / ts * bw;
+      uint8_t* out = arena_alloc(ar, tot ? tot : 1);
+      uint8_t* hdr = arena_alloc(ar, 4 + 4 * (uint64_t)D->np);
+      if (!out || !hdr) return TDBG_E_ARG;
+      st(hdr, (uint64_t)D->np, 4);
+      uint64_t o = 0;
+      for (int i = 0; i < D->np; i++) {
+        uint64_t ne = D->v[i].n / ts;
+        st(hdr + 4 + 4 * i, ne * bw, 4);
+        fscale_fwd(ts, bw, f->scale, f->offset, D->v[i].p, ne, out + o);
+        o += ne * bw;
+      }
+      plist_push(D2, out, tot);
+      return md_prepend(M2, hdr, 4 + 4 * (uint64_t)D->np, M);
+    }
     case TDBG_FILTER_XOR: { /* xor_filter.cc:120-146: one part per input buffer */
       uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype);
       if (ts != 1 && ts != 2 && ts != 4 && ts != 8) return TDBG_E_ARG;
@@ -1135,6 +1213,31 @@ static int rev_filter(const oracle_pipeline* p, const oracle_filter* f,
   switch (f->type) {
     case TDBG_FILTER_NONE:
       PASS_THROUGH();
+    case TDBG_FILTER_SCALE_FLOAT: {
+      /* float_scaling_filter.cc:164-197, 217-238: one output prepend per
+       * part; a fixed allocation allows only the first (filter_buffer.cc:
+       * 508-545); several parts into a growable buffer are not modelled
+       * (TDBG_E_UNSUPPORTED, parity unpinned) */
+      uint32_t ts = (uint32_t)oracle_datatype_size(f->datatype), bw = (uint32_t)f->byte_width;
+      if ((ts != 4 && ts != 8) || (bw != 1 && bw != 2 && bw != 4 && bw != 8))
+        return TDBG_E_UNSUPPORTED;
+      uint32_t np;
+      if ((rc = md_read(md, &np, 4))) return rc;
+      uint64_t ip = 0, op = 0;
+      for (uint32_t i = 0; i < np; i++) {
+        uint32_t ps;
+        if ((rc = md_read(md, &ps, 4))) return rc;
+        if (ip + ps > in_n) return TDBG_E_DATA_READ;
+        uint64_t ne = ps / bw;
+        if (i > 0) return out->fixed ? TDBG_E_OUT_FULL : TDBG_E_UNSUPPORTED;
+        if ((rc = out_prepend(out, ne * ts))) return rc;
+        fscale_rev(ts, bw, f->scale, f->offset, in + ip, ne, out->p);
+        op = ne * ts;
+        ip += ps;
+      }
+      finish_size(out, op);
+      return TDBG_OK;
+    }
     case TDBG_FILTER_BYTESHUFFLE:
     case TDBG_FILTER_BITSHUFFLE:
     case TDBG_FILTER_XOR: {

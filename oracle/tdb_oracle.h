@@ -36,6 +36,8 @@ typedef struct oracle_filter {
   uint8_t reinterpret; /* DD/DELTA reinterpret datatype, ANY if absent      */
   uint32_t window;     /* BWR / PD max window                               */
   uint8_t datatype;    /* filter_data_type_ from the datatype chain         */
+  double scale, offset; /* FLOAT_SCALE FilterConfig (float_scaling_filter.h:61-65) */
+  uint64_t byte_width;
 } oracle_filter;
 
 typedef struct oracle_pipeline {

@@ -16,7 +16,7 @@ import numpy as np
 from tiledb_amd.filter_pipeline import (FORMAT_VERSION, BitshuffleFilter, BitWidthReductionFilter,
                                         ByteshuffleFilter, CompressionFilter, Compressor, Datatype,
                                         FilterPipeline, NoopFilter, PositiveDeltaFilter,
-                                        XORFilter, datatype_size)
+                                        FloatScalingFilter, XORFilter, datatype_size)
 
 
 @dataclass
@@ -317,6 +317,26 @@ def edge_cases() -> List[Case]:
                       I32, 4, [as_u8(np.arange(16384, dtype=np.int32) * 5)]))
     cases.append(Case("delta_multichunk_i64", P(DELTA()), I64, 8,
                       [as_u8(np.cumsum(rng.integers(0, 9, 30000)).astype(np.int64))], max_chunk=8192))
+    # FLOAT_SCALE (float_scaling_filter.cc).  Exact cases:
+    # values on the scale grid (binary scale/offset) round-trip bit-exactly;
+    # lossy cases (decimal scale) are still GPU-vs-oracle bit-exact
+    k = rng.integers(-30000, 30000, 16384)
+    for bw in (2, 4, 8):
+        cases.append(Case(f"fscale_f32_exact_bw{bw}", P(FloatScalingFilter(0.125, -3.0, bw)),
+                          Datatype.FLOAT32, 4, [as_u8((-3.0 + 0.125 * k).astype(np.float32))]))
+    cases.append(Case("fscale_f64_exact_bw8", P(FloatScalingFilter(2.0 ** -20, 1.5, 8)),
+                      Datatype.FLOAT64, 8, [as_u8(1.5 + k.astype(np.float64) * 2.0 ** -20)]))
+    cases.append(Case("fscale_f32_lossy_bw1", P(FloatScalingFilter(0.01, 0.5, 1)), Datatype.FLOAT32, 4,
+                      [as_u8(rng.uniform(-0.7, 1.7, 5000).astype(np.float32))],
+                      extra={"lossy": (np.float32, 0.01)}))
+    cases.append(Case("fscale_f64_lossy_then_bwr",
+                      P(FloatScalingFilter(1e-3, 0.0, 4), BitWidthReductionFilter(256)),
+                      Datatype.FLOAT64, 8, [as_u8(np.sin(np.arange(8192) * 1e-2))],
+                      extra={"lossy": (np.float64, 1e-3)}))
+    cases.append(Case("fscale_f32_then_delta_bitshuffle",
+                      P(FloatScalingFilter(0.5, 0.0, 4), DELTA(), BitshuffleFilter()),
+                      Datatype.FLOAT32, 4, [as_u8((0.5 * np.arange(20000)).astype(np.float32))],
+                      max_chunk=16384))
     return cases
 
 

@@ -122,7 +122,7 @@ def _mutations(f: np.ndarray, rng):
 @pytest.mark.parametrize("case", _CONFIG + [c for c in _EDGE if c.name.startswith(("dd_", "rle_run_65535",
                                                                                     "bwr_window_437",
                                                                                     "pd_", "bwr_then",
-                                                                                    "byte_bit", "xor_",
+                                                                                    "byte_bit", "xor_", "fscale_",
                                                                                     "delta_"))],
                          ids=lambda c: c.name)
 def test_corrupt_tiles_status_parity(eng, ctx, oracle_mod, case):

@@ -271,7 +271,12 @@ def _roundtrip(O, case):
         osz = t.size + (8 if case.offsets_tile else 0)
         rc, out = op.unfilter_tile(f, osz, case.offsets_tile)
         assert rc == 0, (case.name, rc)
-        assert np.array_equal(out[: t.size], t), case.name
+        if "lossy" in case.extra:  # FLOAT_SCALE quantization: |x' - x| <= scale / 2
+            ft, scale = case.extra["lossy"]
+            err = np.abs(out[: t.size].view(ft).astype(np.float64) - t.view(ft).astype(np.float64))
+            assert err.max() <= scale / 2 * (1 + 1e-6) + 1e-6, case.name
+        else:
+            assert np.array_equal(out[: t.size], t), case.name
         n += 1
     return n
 
@@ -398,3 +403,22 @@ def test_delta_known_answer(oracle_mod):
     g[36] = 5
     rc, _ = op.unfilter_tile(g, x.nbytes)
     assert rc == 5  # TDBG_E_DATA_READ
+
+
+def test_float_scale_known_answer(oracle_mod):
+    """FLOAT_SCALE: stored W = round((x - offset) / scale) in T (float_scaling_filter.cc:60-99),
+    read back as T(scale * T(W) + offset) (:164-197); descriptor = FilterConfig (24 B)."""
+    from tiledb_amd.filter_pipeline import FloatScalingFilter
+    x = np.array([1.0, 1.26, -2.5, 100.0], dtype=np.float32)
+    fp = P(FloatScalingFilter(0.5, 1.0, 2))
+    ser = fp.serialize()
+    assert ser[8:13] == bytes([15, 24, 0, 0, 0])
+    assert FilterPipeline.deserialize(ser, 23, Datatype.FLOAT32).serialize() == ser
+    op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.FLOAT32), 4)
+    assert op.serialize() == ser
+    f = np.frombuffer(op.filter_tile(as_u8(x)), dtype=np.uint8)
+    assert f[20:28].view(np.uint32).tolist() == [1, 8]
+    assert f[28:36].view(np.int16).tolist() == [0, 1, -7, 198]   # round(0.52) = 1
+    rc, back = op.unfilter_tile(f, x.nbytes)
+    assert rc == 0
+    assert back.view(np.float32).tolist() == [1.0, 1.5, -2.5, 100.0]

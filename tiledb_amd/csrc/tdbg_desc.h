@@ -21,7 +21,8 @@ enum tdbg_stage_kind : uint8_t {
   TDBG_K_RLE = 6,         // CompressionFilter + RLE::decompress
   TDBG_K_XOR = 7,         // XORFilter::run_reverse<T> (prefix XOR; general interpreter only)
   TDBG_K_DELTA = 8,       // CompressionFilter + Delta::decompress<T> (general interpreter only)
-  TDBG_K_UNSUPPORTED = 9
+  TDBG_K_FSCALE = 9,      // FloatScalingFilter::run_reverse<T, W> (general interpreter only)
+  TDBG_K_UNSUPPORTED = 10
 };
 
 struct tdbg_stage {
@@ -37,6 +38,8 @@ struct tdbg_plan {
   uint32_t nstages;
   uint32_t fast;  // fused fast-path selector (tdbg_fast_kind), 0 = none
   tdbg_stage s[TDBG_MAX_FILTERS];
+  double fs_scale[TDBG_MAX_FILTERS];   // FLOAT_SCALE stages: FilterConfig scale / offset
+  double fs_offset[TDBG_MAX_FILTERS];
 };
 
 #define TDBG_E_FALLBACK 100  // internal status: the fast path declined the tile

@@ -218,6 +218,58 @@ __device__ int g_bwr(StageIO& io, const tdbg_stage& s, Slot& sl, Shared<NT>& sh)
 }
 
 // ---------------------------------------------------------------------------
+// FLOAT_SCALE^-1 (FloatScalingFilter::run_reverse<T, W>,
+// float_scaling_filter.cc:164-197): T(scale * double(T(w)) + offset), the
+// multiply and the add rounded separately (no FMA contraction, as the
+// reference's x86-64 build).  One output prepend per part: a fixed allocation
+// takes only the first (filter_buffer.cc:508-545); several parts into a
+// growable buffer are not modelled (TDBG_E_UNSUPPORTED, as the oracle).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ int g_fscale(StageIO& io, const tdbg_stage& s, double sc, double of) {
+  // hipcc contracts a * b + c into an FMA by default (-ffp-contract=fast),
+  // even through __dmul_rn/__dadd_rn once inlined; the reference rounds the
+  // product and the sum separately (an empty asm on the product pins that)
+  if (io.md_n < 4) return TDBG_E_MD_READ;
+  const uint32_t np = (uint32_t)ldn(io.md, 4);
+  const uint32_t ts = s.dts, bw = s.w;
+  uint64_t ip = 0, op = 0;
+  for (uint32_t i = 0; i < np; i++) {
+    if (4 + 4 * ((uint64_t)i + 1) > io.md_n) return TDBG_E_MD_READ;
+    const uint32_t ps = (uint32_t)ldn(io.md + 4 + 4 * i, 4);
+    if (ip + ps > io.in_n) return TDBG_E_DATA_READ;
+    if (i > 0) return io.fixed ? TDBG_E_OUT_FULL : TDBG_E_UNSUPPORTED;
+    const uint64_t ne = ps / bw, on = ne * ts;
+    if (on > io.cap) {
+      if (io.fixed) return TDBG_E_OUT_FULL;
+      io.need = on;
+      return TDBG_E_SCRATCH;
+    }
+    const uint8_t* src = io.in + ip;
+    for (uint64_t j = threadIdx.x; j < ne; j += NT) {
+      const int64_t q = sext64(ldn(src + j * bw, bw), bw);
+      if (ts == 4) {
+        const float e = __ll2float_rn(q);
+        double prod = sc * (double)e;
+        asm volatile("" : "+v"(prod));  // keeps the product rounded: no v_fma_f64
+        const float y = __double2float_rn(prod + of);
+        stn(io.out + 4 * j, (uint64_t)__float_as_uint(y), 4);
+      } else {
+        double prod = sc * __ll2double_rn(q);
+        asm volatile("" : "+v"(prod));
+        const double y = prod + of;
+        stn(io.out + 8 * j, (uint64_t)__double_as_longlong(y), 8);
+      }
+    }
+    op = on;
+    ip += ps;
+  }
+  io.md_used = 4 + 4 * (uint64_t)np;
+  io.out_n = io.fixed ? io.cap : op;
+  return TDBG_OK;
+}
+
+// ---------------------------------------------------------------------------
 // PD^-1 (positive_delta_filter.cc:324-375)
 // md: [u32 nwin] nwin x [T first][u32 nbytes]
 // ---------------------------------------------------------------------------
@@ -564,6 +616,9 @@ __device__ __attribute__((noinline)) int g_chunk(const tdbg_plan& P, const uint8
         break;
       case TDBG_K_PD:
         rc = g_pd<NT>(io, s, sl, sh);
+        break;
+      case TDBG_K_FSCALE:
+        rc = g_fscale<NT>(io, s, P.fs_scale[k], P.fs_offset[k]);
         break;
       case TDBG_K_DD:
       case TDBG_K_DELTA:

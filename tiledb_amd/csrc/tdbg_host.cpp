@@ -84,6 +84,8 @@ struct Filter {
   uint8_t reinterpret = TDBG_ANY;
   uint32_t window = 0;
   uint8_t datatype = 0;
+  double scale = 1.0, offset = 0.0;  // FLOAT_SCALE FilterConfig (float_scaling_filter.h:61-65)
+  uint64_t byte_width = 8;
 };
 
 uint8_t compressor_filter(uint8_t c) {
@@ -209,6 +211,19 @@ void build_plan(tdbg_pipeline* p) {
         s.kind = TDBG_K_BITSHUFFLE;
         s.w = (uint8_t)dt_size(dt);
         break;
+      case TDBG_FILTER_SCALE_FLOAT: {  // float_scaling_filter.cc:217-238: float/double in
+        const uint64_t ts = dt_size(dt), bw = f.byte_width;
+        if ((ts == 4 || ts == 8) && (bw == 1 || bw == 2 || bw == 4 || bw == 8)) {
+          s.kind = TDBG_K_FSCALE;
+          s.w = (uint8_t)bw;
+          P.fs_scale[i] = f.scale;
+          P.fs_offset[i] = f.offset;
+        } else {
+          s.kind = TDBG_K_UNSUPPORTED;
+          p->supported = false;
+        }
+        break;
+      }
       case TDBG_FILTER_XOR: {  // xor_filter.cc:179-218: integer of the type's width
         const uint64_t w = dt_size(dt);
         if (w == 1 || w == 2 || w == 4 || w == 8) {
@@ -374,6 +389,9 @@ int tdbg_pipeline_create(const uint8_t* b, size_t len, uint32_t version,
         break;
       case TDBG_FILTER_SCALE_FLOAT:
         if (!need(24)) { delete p; return fail(TDBG_E_DESCRIPTOR, "truncated float scale config"); }
+        memcpy(&f.scale, b + o, 8);
+        memcpy(&f.offset, b + o + 8, 8);
+        memcpy(&f.byte_width, b + o + 16, 8);
         o += 24;
         break;
       case TDBG_FILTER_WEBP:
@@ -387,6 +405,15 @@ int tdbg_pipeline_create(const uint8_t* b, size_t len, uint32_t version,
     if ((f.type == TDBG_FILTER_DOUBLE_DELTA || f.type == TDBG_FILTER_DELTA) &&
         f.reinterpret != TDBG_ANY)
       cur = f.reinterpret;  // CompressionFilter::output_datatype
+    if (f.type == TDBG_FILTER_SCALE_FLOAT) {  // float_scaling_filter.cc:313-327
+      switch (f.byte_width) {
+        case 1: cur = TDBG_INT8; break;
+        case 2: cur = TDBG_INT16; break;
+        case 4: cur = TDBG_INT32; break;
+        case 8: cur = TDBG_INT64; break;
+        default: break;  // the reference throws; build_plan marks it unsupported
+      }
+    }
     if (f.type == TDBG_FILTER_XOR) {  // XORFilter::output_datatype xor_filter.cc:63-78
       switch (dt_size(cur)) {
         case 1: cur = TDBG_INT8; break;

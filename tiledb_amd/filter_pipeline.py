@@ -270,6 +270,37 @@ class XORFilter(Filter):
         return m[w]
 
 
+class FloatScalingFilter(Filter):
+    """float_scaling_filter.cc: FilterConfig {double scale, double offset,
+    u64 byte_width} (.h:61-65); accepts 4/8-byte inputs (:306-310); output =
+    the signed integer of byte_width (:313-327)."""
+
+    type = FilterType.FILTER_SCALE_FLOAT
+
+    def __init__(self, scale: float = 1.0, offset: float = 0.0, byte_width: int = 8,
+                 filter_data_type: int = Datatype.ANY):
+        super().__init__(filter_data_type)
+        self.scale, self.offset, self.byte_width = float(scale), float(offset), int(byte_width)
+
+    def serialize_impl(self) -> bytes:
+        return struct.pack("<ddQ", self.scale, self.offset, self.byte_width)
+
+    def accepts_input_datatype(self, datatype: int) -> bool:
+        return datatype_size(datatype) in (4, 8)
+
+    def output_datatype(self, input_type: int) -> Datatype:
+        m = {1: Datatype.INT8, 2: Datatype.INT16, 4: Datatype.INT32, 8: Datatype.INT64}
+        if self.byte_width not in m:
+            raise FilterStatusException(
+                "FloatScalingFilter::output_datatype: byte_width_ does not reflect the size of "
+                "an integer type.")
+        return m[self.byte_width]
+
+    def __repr__(self) -> str:
+        return (f"ScaleFloat: SCALE_FLOAT_BYTEWIDTH={self.byte_width}, "
+                f"SCALE_FLOAT_FACTOR={self.scale}, SCALE_FLOAT_OFFSET={self.offset}")
+
+
 class CompressionFilter(Filter):
     """compression_filter.cc.  The filter type follows the compressor."""
 
@@ -411,6 +442,10 @@ class FilterPipeline:
                 f = ByteshuffleFilter(dt)
             elif ftype == FilterType.FILTER_XOR:
                 f = XORFilter(dt)
+            elif ftype == FilterType.FILTER_SCALE_FLOAT:
+                sc, of, bw = struct.unpack_from("<ddQ", data, o)
+                o += 24
+                f = FloatScalingFilter(sc, of, bw, dt)
             else:
                 o += mdlen
                 f = Filter(dt)
