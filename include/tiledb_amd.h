@@ -205,8 +205,10 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
 int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
                        uint64_t* read_unfiltered_byte_num);
 
-/* Device-side timing of the last tdbg_unfilter_tiles_* launch on ctx, via
- * hipEvents recorded around the kernel on its stream (ms). */
+/* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on
+ * ctx (fused/general kernel + fixup), from the hipEvents that
+ * tdbg_context_time_launches arms.  Un-armed launches record no events: an
+ * event record costs ~3 % of a C5 launch on the stream's timeline. */
 int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
 
 /* Per-launch device timing for benchmarks: arm event recording for the next

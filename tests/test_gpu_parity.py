@@ -244,6 +244,7 @@ def test_async_api_and_timing(eng, ctx, oracle_mod):
     _, enc = encode(oracle_mod, case)
     dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     batch = eng.TileBatch.from_host([e[0] for e in enc], [e[2] for e in enc])
+    ctx.time_launches(1)  # events only on armed launches
     ctx.unfilter_async(dp, batch)
     torch.cuda.synchronize()
     assert not batch.d_status.cpu().numpy().any()
