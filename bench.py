@@ -4,12 +4,16 @@
 Workload (BASELINE.json configs[4]): dense int32 tiles of
 64 KiB (one chunk each), pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)],
 12,500 tiles per GPU (C5's 100k tiles over 8 GPUs; weak scaling).  The other
-configs run with --config c1|c2|c2i|c3a|c3b|c4 (parity-test cases; not the
-headline line).  A step is
-one unfilter pass (one tdbg_unfilter_tiles_async launch) over the rank's
-12,500 resident tiles.  The headline `value` is the "rand" data variant
-(every byte moves; DD falls back to raw); the "ramp" variant is reported
-beside it.
+configs run with --config c1|c2|c2i|c3a|c3b|c4 (one JSON line each).  A step
+is one unfilter pass (one tdbg_unfilter_tiles_async launch) over the rank's
+12,500 resident tiles, packed back to back in HBM at arbitrary byte offsets
+(as FilteredData hands them over, filtered_data.h:100-101).
+
+The headline `value` is the "active" data variant, the one where all three
+stages do work (DoubleDelta bit-packed, BWR windows 8-bit, byteshuffle);
+"rand" (DD and BWR raw: two stages are views) and "ramp" (DD raw) are
+reported beside it, with the minimum over the three.  Every timed launch's
+statuses and every output tile are checked after the timed region.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
@@ -46,21 +50,20 @@ CONFIGS = {
     "c4": dict(tiles_per_gpu=12500, variants="offsets", dtype="uint64",
                workload="C4: var-length offsets uint64, [POSITIVE_DELTA(1024), BIT_WIDTH_REDUCTION(256)], "
                         "50k tiles / 4 GPUs"),
-    "c5": dict(tiles_per_gpu=12500, variants="rand,ramp", dtype="int32",
+    "c5": dict(tiles_per_gpu=12500, variants="active,rand,ramp", dtype="int32",
                workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
                         "64 KiB tiles (1 chunk), device-resident, 100k tiles / 8 GPUs"),
 }
 
 
-def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, device: int, seed: int):
+def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, device: int, seed: int,
+                align: int = 1):
     import workloads as W
     pool, vals = W.pool(cfg, variant, nunique, seed)
     idx = np.arange(ntiles) % nunique
     sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
-    al = (sizes + np.uint64(15)) // np.uint64(16) * np.uint64(16)
-    offs = np.zeros_like(sizes)
-    offs[1:] = np.cumsum(al)[:-1]
-    packed = np.zeros(int(al.sum()), dtype=np.uint8)
+    offs = engine.pack_offsets(sizes, align)
+    packed = np.zeros(int(offs[-1] + sizes[-1]), dtype=np.uint8)
     pool_np = [np.frombuffer(p, dtype=np.uint8) for p in pool]
     for k, (i, o) in enumerate(zip(idx, offs)):
         packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
@@ -70,16 +73,18 @@ def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, devic
 
 
 def verify(batch, vals, idx) -> None:
-    """Every distinct source tile's first occurrence equals its values."""
-    first = {}
-    for t, i in enumerate(idx):
-        if i not in first:
-            first[i] = t
-    for i, t in first.items():
-        o, n = int(batch.out_off[t]), int(batch.out_size[t])
-        got = batch.d_out[o:o + n].cpu().numpy()
-        if not np.array_equal(got, vals[i].view(np.uint8)):
-            raise SystemExit(f"bench verification failed: tile {t} differs from its source values")
+    """Every output tile equals its source values (compared on the device)."""
+    import torch
+    nb = int(vals[0].nbytes)
+    if any(int(v.nbytes) != nb for v in vals) or (batch.out_size != nb).any():
+        raise SystemExit("bench verification assumes equal tile sizes")
+    uniq = torch.from_numpy(np.stack([v.view(np.uint8) for v in vals])).to(batch.d_out.device)
+    got = batch.d_out[: batch.ntiles * nb].view(batch.ntiles, nb)
+    exp_idx = torch.from_numpy(np.asarray(idx, dtype=np.int64)).to(batch.d_out.device)
+    bad = (got != uniq[exp_idx]).any(dim=1)
+    if bool(bad.any()):
+        t = int(torch.nonzero(bad)[0])
+        raise SystemExit(f"bench verification failed: tile {t} differs from its source values")
 
 
 def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: int):
@@ -95,6 +100,8 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     if st.any():
         raise SystemExit(f"device status nonzero: {np.unique(st)}")
     ctx.time_launches(steps)
+    fused0, fb0, _ = ctx.path_stats()
+    batch.d_status.fill_(-1)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -106,9 +113,15 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, total_ms = ctx.launch_times(steps)
+    # after the timed region: every launch wrote status OK for every tile,
+    # and the fused kernel took every tile of every timed launch
+    st = batch.d_status[: batch.ntiles].cpu().numpy()
+    if st.any():
+        raise SystemExit(f"timed launches: device status nonzero: {np.unique(st)}")
+    fused1, fb1, _ = ctx.path_stats()
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, "cuda")
-    return elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms))
+    return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0)
 
 
 def max_over_ranks(dist, x: float, device: str) -> float:
@@ -119,23 +132,33 @@ def max_over_ranks(dist, x: float, device: str) -> float:
     return float(t.item())
 
 
-def cpu_baseline(cfg, packed, offs, sizes, out_bytes, ntiles_sample: int, threads: int,
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(engine, dp, packed, offs, sizes, out_bytes, ntiles_sample: int, threads: int,
                  min_seconds: float = 10.0):
-    """Oracle (CPU restatement, test infrastructure) on a bounded sample."""
-    from oracle import oracle as O
-    import workloads as W
-    ser, dt, cs, _, _ = W.config(cfg)
-    op = O.OraclePipeline(ser, 23, int(dt), cs)
+    """The engine's CPU entry (tdbg_unfilter_tiles_cpu: C++ restatement of the
+    reverse pipeline with the reference's tile x chunk-range thread split,
+    reader_base.cc:929-989) on a bounded sample of the same tiles."""
     n = min(ntiles_sample, offs.size)
     out = np.zeros(n * out_bytes, dtype=np.uint8)
-    out_off = np.arange(n, dtype=np.uint64) * np.uint64(out_bytes)
+    in_ptrs = offs[:n] + np.uint64(packed.ctypes.data)
+    out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(out_bytes) + np.uint64(out.ctypes.data)
     out_size = np.full(n, out_bytes, dtype=np.uint64)
     reps = 0
     t0 = time.perf_counter()
     while True:
-        rc, st = op.unfilter_tiles_mt(packed, offs[:n], sizes[:n], out, out_off, out_size, threads)
-        if rc:
-            raise SystemExit(f"cpu baseline failed: {rc}")
+        st = engine.unfilter_cpu(dp, in_ptrs, sizes[:n], out_ptrs, out_size, nthreads=threads)
+        if st.any():
+            raise SystemExit(f"cpu baseline failed: {np.unique(st)}")
         reps += 1
         el = time.perf_counter() - t0
         if el >= min_seconds:
@@ -144,13 +167,18 @@ def cpu_baseline(cfg, packed, offs, sizes, out_bytes, ntiles_sample: int, thread
     return gib / el, reps * n, el
 
 
-def load_traffic(variant: str):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+TRAFFIC_FILE = "profiles/pmc_traffic.json"
+
+
+def load_traffic(cfg: str, variant: str):
+    """HBM bytes per launch of the same workload from the committed rocprofv3
+    --pmc FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh): not measured in this
+    run (PMC counters need their own rocprofv3 passes)."""
+    path = os.path.join(ROOT, TRAFFIC_FILE)
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(variant, {}).get("hbm_bytes_per_launch")
+        return d.get(f"{cfg}_{variant}", {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -166,8 +194,11 @@ def main():
                     help="default: the config's per-GPU tile count (C5: 100k / 8)")
     ap.add_argument("--unique", type=int, default=128)
     ap.add_argument("--variants", default="")
+    ap.add_argument("--align", type=int, default=1,
+                    help="tile start alignment in HBM (1 = back to back, as on disk)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", default=True,
                     help="also time host-resident end-to-end (default on; every rank, "
                          "total over ranks / max-over-ranks time)")
@@ -200,30 +231,39 @@ def main():
     res = {}
     for vi, var in enumerate(variants):
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
-            engine, args.config, var, ntiles, args.unique, local, seed=5 + 1000 * rank + vi)
-        ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
+            engine, args.config, var, ntiles, args.unique, local, seed=5 + 1000 * rank + vi,
+            align=args.align)
+        st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
+        if st.any():
+            raise SystemExit(f"{var}: first pass status nonzero: {np.unique(st)}")
+        verify(batch, vals, idx)
+        elapsed, kern_ms, launch_ms, fused, fallback = time_device(
+            engine, ctx, dp, batch, args.steps, args.warmup, dist, world)
         if not os.environ.get("TDBG_DEBUG_STOP"):  # timing-only ablation skips output checks
             verify(batch, vals, idx)
-        elapsed, kern_ms, launch_ms = time_device(engine, ctx, dp, batch, args.steps,
-                                                  args.warmup, dist, world)
-        kname = "unfilter_fused_kernel"
         unf = float(sum(vals[i].nbytes for i in idx))
         b_alg = float(sizes.sum()) + unf
-        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, kname=kname, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
-                        out_bytes=int(vals[0].nbytes),
+        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
+                        out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback,
                         packed=packed, offs=offs, sizes=sizes)
         if args.e2e:
-            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, args, dist, world)
+            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args,
+                                  dist, world)
         del batch
         torch.cuda.empty_cache()
+
+    def gibps(r):
+        return r["unf"] * world / (r["elapsed"] / args.steps) / 2**30
+
+    def frac(r):
+        return r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
 
     head = variants[0]
     r = res[head]
     ms_per_step = r["elapsed"] / args.steps * 1e3
-    total_unf = r["unf"] * world
-    value = total_unf / (r["elapsed"] / args.steps) / 2**30
+    value = gibps(r)
     achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
-    traffic = load_traffic(head) if args.config == "c5" else None
+    traffic = load_traffic(args.config, head)
     line = {
         "metric": "GiB/s unfiltered tile bytes (device-resident), 64 KiB chunks, 3-stage pipeline",
         "value": round(value, 2),
@@ -242,8 +282,11 @@ def main():
             "workload": cfg["workload"],
             "tiles_per_gpu": ntiles,
             "variant": head,
+            "tile_alignment": args.align,
             "parallelism": f"tile-shard x{world} (no collectives)",
             "filtered_bytes_per_gpu": int(r["sizes"].sum()),
+            "fused_tiles_timed": r["fused"],
+            "fallback_tiles_timed": r["fallback"],
         },
         "roofline": {
             "bound": "hbm",
@@ -252,31 +295,34 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": r["kname"],
+            "traffic_source": f"{TRAFFIC_FILE} (committed rocprofv3 --pmc passes of this workload)"
+                              if traffic else None,
+            "kernel": "unfilter_fused_kernel",
             "kernel_ms": round(r["kern_ms"], 4),
             "launch_ms": round(r["launch_ms"], 4),
             "algorithmic_bytes_per_launch": int(r["b_alg"]),
         },
     }
-    for var in variants[1:]:
-        rv = res[var]
-        line["config"][f"{var}_GiBps"] = round(
-            rv["unf"] * world / (rv["elapsed"] / args.steps) / 2**30, 2)
-        line["config"][f"{var}_roofline_frac"] = round(
-            rv["b_alg"] / (rv["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if len(variants) > 1:
+        line["config"]["variants"] = {
+            v: {"GiBps": round(gibps(res[v]), 2), "roofline_frac": round(frac(res[v]), 4),
+                "kernel_ms": round(res[v]["kern_ms"], 4), "fallback_tiles_timed": res[v]["fallback"]}
+            for v in variants}
+        line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v]) for v in variants), 2)
     if args.e2e:
         line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        cpu, ntl, el = cpu_baseline(args.config, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
-                                    2048, threads)
+        cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
+                                    2048, threads, args.cpu_seconds)
         line["cpu_baseline"] = {
             "value": round(cpu, 3),
             "unit": "GiB/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"{ntl} {args.config.upper()} '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s on "
-                      f"{threads} threads, oracle/ C restatement",
+            "sample": f"{ntl} {args.config.upper()} '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s "
+                      f"on {threads} threads of '{cpu_model()}' ({os.cpu_count()} CPUs visible), "
+                      "tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry)",
         }
     if rank == 0:
         print(json.dumps(line))
@@ -284,31 +330,33 @@ def main():
         dist.destroy_process_group()
 
 
-def e2e(engine, ctx, dp, packed, offs, sizes, args, dist=None, world=1):
+def e2e(engine, ctx, dp, packed, offs, sizes, out_bytes, args, dist=None, world=1):
     """Host-resident end-to-end: pinned H2D + unfilter + D2H (PCIe-inclusive).
     Every rank moves its own tiles through its own GPU's link; the rate is the
-    total over ranks / the slowest rank's time (not `value`: DESIGN.md)."""
+    total over ranks / the slowest rank's time (not `value`: DESIGN.md).  The
+    filtered tiles sit back to back in one pinned block (a FilteredData-style
+    batch) and the results in one pinned result buffer."""
     import torch
-    import workloads as W
     n = offs.size
     hin = torch.from_numpy(packed).pin_memory()
-    hout = torch.empty(n * W.TILE_BYTES, dtype=torch.uint8).pin_memory()
+    hout = torch.empty(n * out_bytes, dtype=torch.uint8).pin_memory()
     in_ptrs = offs + np.uint64(hin.data_ptr())
-    out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES) + np.uint64(hout.data_ptr())
-    osz = np.full(n, W.TILE_BYTES, dtype=np.uint64)
+    out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(out_bytes) + np.uint64(hout.data_ptr())
+    osz = np.full(n, out_bytes, dtype=np.uint64)
     bb = args.e2e_batch_mb << 20
-    ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=bb)
+    kw = dict(batch_bytes=bb, contiguous_input=True, contiguous_output=True)
+    ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, **kw)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     reps = 3
     for _ in range(reps):
-        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, batch_bytes=bb)
+        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz, **kw)
     el = time.perf_counter() - t0
     assert not st.any()
     if dist is not None:
         el = max_over_ranks(dist, el, "cuda")
-    return round(world * reps * n * W.TILE_BYTES / el / 2**30, 2)
+    return round(world * reps * n * out_bytes / el / 2**30, 2)
 
 
 if __name__ == "__main__":

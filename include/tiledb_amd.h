@@ -108,11 +108,21 @@ enum tdbg_status {
   TDBG_E_PD_DECREASING = 12,/* forward only: "delta is not positive"           */
   TDBG_E_DD_OVERFLOW = 13,  /* forward only: delta exceeds int64               */
   TDBG_E_DEVICE = 14,       /* HIP runtime error                               */
-  TDBG_E_DESCRIPTOR = 15    /* malformed serialized pipeline                    */
+  TDBG_E_DESCRIPTOR = 15,   /* malformed serialized pipeline                    */
+  TDBG_E_DELTA_TYPE = 16    /* Delta float: "Decompression is not yet supported for
+                               float datatypes." delta_compressor.cc:210-213   */
 };
 
 /* unfilter flags */
 #define TDBG_TILE_OFFSETS 0x1u /* offsets tile: expected size = out_size - 8 (tile.cc:241-248) */
+/* tdbg_unfilter_tiles_host only: every input tile of the call lies in ONE host
+ * allocation (e.g. a FilteredData block, filtered_data.h:152-644), so tiles
+ * separated by at most 64 B of padding may move in one H2D copy (padding
+ * included).  Without it every tile is its own copy. */
+#define TDBG_HOST_CONTIGUOUS_INPUT 0x2u
+/* tdbg_unfilter_tiles_host only: every output buffer lies in one host
+ * allocation; exactly adjacent outputs may share one D2H copy. */
+#define TDBG_HOST_CONTIGUOUS_OUTPUT 0x4u
 
 typedef struct tdbg_pipeline tdbg_pipeline; /* immutable, shareable */
 typedef struct tdbg_context tdbg_context;   /* per (device, host thread) */
@@ -131,16 +141,25 @@ int tdbg_pipeline_create(const uint8_t* serialized, size_t len,
                          uint32_t format_version, uint8_t on_disk_datatype,
                          uint64_t cell_size, tdbg_pipeline** out);
 void tdbg_pipeline_destroy(tdbg_pipeline* p);
-/* 1 if every filter runs on the engine, 0 if the caller must keep its own CPU
- * path (checksum, encryption, gzip/zstd/lz4/bzip2, dictionary, xor, float
- * scale, webp, delta). */
+/* 1 if every filter runs on the engine, 0 if the caller must keep its own
+ * path.  Supported: NONE/NOOP, BYTESHUFFLE, BITSHUFFLE, BIT_WIDTH_REDUCTION,
+ * POSITIVE_DELTA, XOR (1/2/4/8-byte types), SCALE_FLOAT (float32/64 input,
+ * byte width 1/2/4/8), and the compression filters NONE, RLE (fixed-size
+ * cells), DOUBLE_DELTA and DELTA.  Unsupported (returns 0): checksums
+ * (MD5/SHA256), AES-256-GCM, GZIP/ZSTD/LZ4/BZIP2, DICTIONARY, WEBP, RLE with
+ * cell size 0, XOR / SCALE_FLOAT on widths the reference rejects. */
 int tdbg_pipeline_supported(const tdbg_pipeline* p);
 uint32_t tdbg_pipeline_num_filters(const tdbg_pipeline* p);
 /* Filter i: type code and the datatype assigned by the chain. */
 int tdbg_pipeline_filter(const tdbg_pipeline* p, uint32_t i, uint8_t* type,
                          uint8_t* datatype);
 
-/* Per-device execution context (scratch, status arrays, streams). */
+/* Per-device execution context (scratch, status arrays, streams).
+ * Threading: the reference is re-entrant (reader_base.cc:929-934); here
+ * each host thread uses its own context (contexts share nothing but the
+ * immutable pipeline).  One context's launches are serialized: a launch on a
+ * different stream than the context's previous launch first waits (on the
+ * host) for that stream. */
 int tdbg_context_create(int device, tdbg_context** out);
 void tdbg_context_destroy(tdbg_context* ctx);
 
@@ -200,10 +219,35 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   int32_t* host_status, const int* devices,
                                   int ndevices, uint64_t batch_bytes);
 
+/* CPU entry: the same batch unfilter on host threads, for
+ * host-resident tiles and the CPU baseline.  The work split is the
+ * reference's: parallel_for_2d over (tile, range thread) with
+ * num_range_threads = ceil(nthreads / ntiles) when ntiles < nthreads, each
+ * range thread taking the chunk range compute_chunk_min_max gives it
+ * (reader_base.cc:929-989, reader_base.h:185-210).  nthreads = 0: hardware
+ * concurrency (sm.compute_concurrency_level's default, config.cc:128-131).
+ * Per-tile statuses as the device path; returns the first failing tile's. */
+int tdbg_unfilter_tiles_cpu(const tdbg_pipeline* p, uint64_t ntiles,
+                            const uint8_t* const* filtered,
+                            const uint64_t* filtered_size, uint8_t* const* out,
+                            const uint64_t* out_size, uint32_t flags,
+                            int32_t* host_status, uint32_t nthreads);
+
 /* Stats mirrored from the reference (filter_pipeline.cc:490-491,
- * reader_base.cc:1074): cumulative since context creation. */
+ * reader_base.cc:1074): cumulative since context creation.  tiles_unfiltered
+ * counts tiles submitted; read_unfiltered_byte_num counts the unfiltered bytes
+ * of tiles that unfiltered successfully (device counters; synchronizes the
+ * device). */
 int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
                        uint64_t* read_unfiltered_byte_num);
+
+/* Which device path handled the tiles (cumulative, synchronizes the device):
+ * fused_tiles = unfiltered by the fused LDS kernel, fallback_tiles = declined
+ * by it and re-run by the general interpreter, general_tiles = unfiltered by
+ * the general interpreter (fallbacks, pipelines without a fused spec and
+ * scratch retries). */
+int tdbg_context_path_stats(const tdbg_context* ctx, uint64_t* fused_tiles,
+                            uint64_t* fallback_tiles, uint64_t* general_tiles);
 
 /* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on
  * ctx (fused/general kernel + fixup), from the hipEvents that

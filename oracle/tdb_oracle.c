@@ -673,7 +673,7 @@ static int delta_compress(uint8_t dtype, const uint8_t* in, uint64_t n,
                           uint8_t* out, uint64_t cap, uint64_t* out_n) {
   ival_t t;
   int rc = dd_type(dtype, &t);
-  if (rc) return rc;
+  if (rc) return rc == TDBG_E_DD_TYPE ? TDBG_E_DELTA_TYPE : rc; /* :210-213 */
   uint64_t num = n / t.w;
   if (cap < 8 + (num ? num : 1) * t.w) return TDBG_E_ARG;
   memcpy(out, &num, 8);
@@ -689,7 +689,7 @@ static int delta_decompress_w(uint8_t dtype, const uint8_t* in, uint64_t n,
   ival_t t;
   *written = 0;
   int rc = dd_type(dtype, &t);
-  if (rc) return rc;
+  if (rc) return rc == TDBG_E_DD_TYPE ? TDBG_E_DELTA_TYPE : rc; /* :210-213 */
   uint64_t num = 0;
   if (n < 8) return TDBG_E_DATA_READ;
   memcpy(&num, in, 8);

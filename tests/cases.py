@@ -388,3 +388,71 @@ def random_cases(n: int, seed: int = 1234, max_elems: int = 3000) -> List[Case]:
         mc = int(rng.choice([0, 0, 1024, 4096]))
         out.append(Case(f"random_{k}", P(*filters), dt, cell, [data], max_chunk=mc))
     return out
+
+
+# ---------------------------------------------------------------------------
+# one case per fused-kernel spec (tdbg_fast.hip SPECS): tiles the fused LDS
+# kernel must take without declining (single 64 KiB chunks, encoder-uniform
+# windows), so tests can assert the fallback counter stays 0
+# ---------------------------------------------------------------------------
+def fused_spec_cases(ntiles: int = 3) -> List[Case]:
+    rng = np.random.default_rng(21)
+    I16, I32, U32, I64, U64 = (Datatype.INT16, Datatype.INT32, Datatype.UINT32, Datatype.INT64,
+                               Datatype.UINT64)
+    F32, F64 = Datatype.FLOAT32, Datatype.FLOAT64
+    B, T, W = ByteshuffleFilter, BitshuffleFilter, BitWidthReductionFilter
+
+    def smooth(dt, n, k):
+        """slowly varying values (BWR windows narrow, DD compresses)."""
+        base = np.cumsum(rng.integers(0, 40, n)).astype(np.int64) + 1000 * k
+        np_t = {I16: np.int16, I32: np.int32, U32: np.uint32, I64: np.int64, U64: np.uint64}[dt]
+        return as_u8(base.astype(np_t))
+
+    def tiles(dt, nbytes=65536):
+        sz = datatype_size(dt)
+        return [smooth(dt, nbytes // sz, k) for k in range(ntiles)]
+
+    def rand(nbytes=65536):
+        return [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(ntiles)]
+
+    def small64(k):
+        """64-bit values whose every byte is < 0x40: the byteshuffled planes read
+        as 64-bit words stay below 2^62, so DoubleDelta's checked deltas cannot
+        overflow (dd_compressor.cc:281-294) and the C5 shape encodes."""
+        a = rng.integers(0, 0x40, (8192, 8), dtype=np.uint8)
+        a[:, 2:] = 0
+        a[:, 0] = (np.arange(8192) // 7 + k) % 0x40
+        return a.reshape(-1)
+
+    f64 = [as_u8(np.sin(np.arange(8192) * 1e-3 + k)) for k in range(ntiles)]
+    out = [
+        Case("spec01_byte_i32", P(B()), I32, 4, tiles(I32) + rand()),
+        Case("spec02_byte_i64", P(B()), I64, 8, tiles(I64) + rand()),
+        Case("spec03_byte_i16", P(B()), I16, 2, tiles(I16) + rand()),
+        Case("spec04_bit_pass_f32", P(T(), W(256)), F32, 4, c2_tiles(ntiles)),
+        Case("spec05_bit_pass_f64", P(T(), W(256)), F64, 8, f64),
+        Case("spec06_bit_i32", P(T()), I32, 4, tiles(I32)),
+        Case("spec07_bit_u64", P(T()), U64, 8, tiles(U64)),
+        Case("spec08_bit_bwr_i32", P(T(), W(256)), I32, 4, tiles(I32) + rand()),
+        Case("spec09_bit_bwr_u32", P(T(), W(256)), U32, 4, tiles(U32)),
+        Case("spec10_bit_bwr_i64", P(T(), W(256)), I64, 8, tiles(I64)),
+        Case("spec11_bit_bwr_u64", P(T(), W(256)), U64, 8, tiles(U64) + rand()),
+        Case("spec12_dd_u64", P(DD()), U64, 8, c3_tiles(ntiles)),
+        Case("spec13_dd_i32", P(DD()), I32, 4, tiles(I32)),
+        Case("spec14_rle_u64", P(RLE()), U64, 8, c3_tiles(ntiles)),
+        Case("spec15_pd_bwr_u64", P(PositiveDeltaFilter(1024), W(256)), U64, 8, c4_tiles(ntiles)),
+        Case("spec16_pd_bwr_i64", P(PositiveDeltaFilter(1024), W(256)), I64, 8, tiles(I64)),
+        Case("spec17_pd_bwr_u32", P(PositiveDeltaFilter(512), W(256)), U32, 4, tiles(U32)),
+        Case("spec18_pd_bwr_i32", P(PositiveDeltaFilter(1024), W(256)), I32, 4, tiles(I32)),
+        Case("spec19_c5_i32", P(B(), DD(), W(256)), I32, 4, c5_tiles(ntiles, "ramp") + c5_tiles(ntiles, "rand")
+             + tiles(I32)),
+        Case("spec20_c5_u32", P(B(), DD(), W(256)), U32, 4, tiles(U32)),
+        Case("spec21_c5_i64", P(B(), DD(), W(256)), I64, 8, [small64(k) for k in range(ntiles)]),
+        Case("spec22_c5_u64", P(B(), DD(), W(256)), U64, 8, [small64(k) for k in range(ntiles)]),
+        Case("spec23_dd_bwr_i64", P(DD(), W(256)), I64, 8, tiles(I64)),
+        Case("spec24_dd_bwr_u64", P(DD(), W(256)), U64, 8, tiles(U64)),
+        Case("spec25_bwr_i32", P(W(256)), I32, 4, tiles(I32) + rand()),
+        Case("spec26_bwr_u64", P(W(256)), U64, 8, tiles(U64)),
+        Case("spec27_bwr_i64", P(W(256)), I64, 8, tiles(I64) + rand()),
+    ]
+    return out

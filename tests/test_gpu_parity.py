@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from tests.cases import config_cases, edge_cases, random_cases
+from tests.cases import config_cases, edge_cases, fused_spec_cases, random_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -41,11 +41,13 @@ def encode(O, case):
     return op, enc
 
 
-def check_parity(eng, ctx, O, case, filtered, out_sizes, originals=None, fill=0):
+def check_parity(eng, ctx, O, case, filtered, out_sizes, originals=None, fill=0, align=1):
+    """Tiles packed back to back by default (align=1): arbitrary tile starts,
+    as FilteredData::data_at hands them over (filtered_data.h:100-101)."""
     op = O.OraclePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     assert dp.supported
-    batch = eng.TileBatch.from_host(filtered, out_sizes, fill=fill)
+    batch = eng.TileBatch.from_host(filtered, out_sizes, fill=fill, align=align)
     st = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile)
     out = batch.outputs_host()
     for i, f in enumerate(filtered):
@@ -70,12 +72,39 @@ _EDGE = edge_cases()
 _RANDOM = random_cases(120)
 
 
+_SPECS = fused_spec_cases(3)
+
+
+@pytest.mark.parametrize("align", [1, 16])
 @pytest.mark.parametrize("case", _CONFIG, ids=[c.name for c in _CONFIG])
-def test_config_parity(eng, ctx, oracle_mod, case):
+def test_config_parity(eng, ctx, oracle_mod, case, align):
+    """BASELINE configs, back-to-back and 16-B aligned tile starts; every tile
+    is taken by the fused kernel (fallback counter unchanged)."""
     _, enc = encode(oracle_mod, case)
     assert enc
+    f0, b0, _ = ctx.path_stats()
     check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc],
-                 [e[1] for e in enc])
+                 [e[1] for e in enc], align=align)
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0, f"{case.name}: {b1 - b0} tiles fell back to the general path"
+    assert f1 - f0 == len(enc)
+
+
+@pytest.mark.parametrize("align", [1, 16])
+@pytest.mark.parametrize("case", _SPECS, ids=[c.name for c in _SPECS])
+def test_fused_spec_no_fallback(eng, ctx, oracle_mod, case, align):
+    """One case per fused-kernel spec (tdbg_fast.hip SPECS): bit-exact, and
+    the fused kernel handled every tile (fallback == 0)."""
+    _, enc = encode(oracle_mod, case)
+    assert len(enc) == len(case.tiles)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    f0, b0, _ = ctx.path_stats()
+    check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc],
+                 [e[1] for e in enc], align=align)
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0, f"{case.name}: {b1 - b0} tiles fell back to the general path"
+    assert f1 - f0 == len(enc)
+    del dp
 
 
 @pytest.mark.parametrize("case", _EDGE, ids=[c.name for c in _EDGE])
@@ -142,26 +171,106 @@ def test_wrong_output_size(eng, ctx, oracle_mod):
     check_parity(eng, ctx, oracle_mod, case, [f, f, f], [osz - 4, osz + 4, 0])
 
 
-def test_full_size_c5_roundtrip(eng, ctx, oracle_mod):
-    """BASELINE C5 per-GPU shard (12,500 tiles x 64 KiB), ramp+rand mixed:
-    size-independent property = the unfiltered bytes equal the written tiles."""
+@pytest.mark.parametrize("align", [1, 16])
+def test_full_size_c5_roundtrip(eng, ctx, oracle_mod, align):
+    """BASELINE C5 per-GPU shard (12,500 tiles x 64 KiB), ramp+rand+active
+    mixed, tiles back to back (align=1) or 16-B aligned: size-independent
+    property = the unfiltered bytes equal the written tiles; every tile taken
+    by the fused kernel."""
+    import workloads as W
     from tests.cases import c5_tiles, P, DD
     from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
     case_p = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
     op = oracle_mod.OraclePipeline(case_p.serialize(), 23, int(Datatype.INT32), 4)
-    uniq = c5_tiles(48, "ramp") + c5_tiles(16, "rand")
+    rng = np.random.default_rng(9)
+    uniq = (c5_tiles(40, "ramp") + c5_tiles(16, "rand") +
+            [W.c5_values("active", k, rng).view(np.uint8) for k in range(16)])
     enc = [np.frombuffer(op.filter_tile(t), dtype=np.uint8) for t in uniq]
     ntiles = 12500
     idx = np.arange(ntiles) % len(enc)
     tiles = [enc[i] for i in idx]
     dp = eng.DevicePipeline(case_p.serialize(), 23, int(Datatype.INT32), 4)
-    batch = eng.TileBatch.from_host(tiles, [65536] * ntiles)
+    batch = eng.TileBatch.from_host(tiles, [65536] * ntiles, align=align)
+    f0, b0, _ = ctx.path_stats()
     st = ctx.unfilter(dp, batch)
+    f1, b1, _ = ctx.path_stats()
     assert not st.any()
+    assert b1 - b0 == 0 and f1 - f0 == ntiles
     out = batch.outputs_host().reshape(ntiles, 65536)
     for k in range(len(enc)):
         rows = out[idx == k]
         assert (rows == uniq[k][None, :]).all()
+
+
+def test_two_contexts_two_threads(eng, oracle_mod):
+    """Two host threads, each with its own context and stream, unfilter
+    concurrently through the C-ABI (the reference is re-entrant,
+    reader_base.cc:929-934)."""
+    import threading
+    import torch
+    errs = []
+
+    def run(case):
+        try:
+            c = eng.Context(0)
+            s = torch.cuda.Stream()
+            _, enc = encode(oracle_mod, case)
+            for _ in range(4):
+                with torch.cuda.stream(s):
+                    check_parity(eng, c, oracle_mod, case, [e[0] for e in enc] * 8, [e[2] for e in enc] * 8)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(c,)) for c in (_CONFIG[0], _CONFIG[-1], _CONFIG[6])]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+
+
+def test_one_context_two_streams(eng, oracle_mod):
+    """Async launches of one context on two streams: the context serializes
+    them (its scratch slots and fallback queue are shared), so both batches
+    come out right, including a batch whose tiles all fall back."""
+    import torch
+    c = eng.Context(0)
+    case = _CONFIG[-2]
+    _, enc = encode(oracle_mod, case)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    mc = next(x for x in _EDGE if x.name == "multichunk_c5_small_chunks")
+    _, enc2 = encode(oracle_mod, mc)
+    dp2 = eng.DevicePipeline(mc.serialized, mc.version, int(mc.dtype), mc.cell_size)
+    b1 = eng.TileBatch.from_host([e[0] for e in enc] * 64, [e[2] for e in enc] * 64)
+    b2 = eng.TileBatch.from_host([e[0] for e in enc2] * 16, [e[2] for e in enc2] * 16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        c.unfilter_async(dp, b1, stream=s1.cuda_stream)
+        c.unfilter_async(dp2, b2, stream=s2.cuda_stream)
+        c.unfilter_async(dp, b1, stream=s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert not b1.d_status.cpu().numpy().any() and not b2.d_status.cpu().numpy().any()
+    o1, o2 = b1.outputs_host(), b2.outputs_host()
+    for i in range(b1.ntiles):
+        e = enc[i % len(enc)]
+        assert np.array_equal(o1[int(b1.out_off[i]):int(b1.out_off[i]) + e[1].size], e[1])
+    for i in range(b2.ntiles):
+        e = enc2[i % len(enc2)]
+        assert np.array_equal(o2[int(b2.out_off[i]):int(b2.out_off[i]) + e[1].size], e[1])
+
+
+def test_scratch_retry_does_not_inflate_context(eng, oracle_mod):
+    """An oversized chunk (1 MiB RLE chunk: TDBG_E_SCRATCH, retried with
+    bigger retry-only slots), then a normal BASELINE-size launch on the same
+    context: both succeed."""
+    c = eng.Context(0)
+    big = next(x for x in _EDGE if x.name == "rle_run_70030")
+    check_parity(eng, c, oracle_mod, big, *[[e[i] for e in encode(oracle_mod, big)[1]] for i in (0, 2)])
+    case = _CONFIG[-1]
+    _, enc = encode(oracle_mod, case)
+    n = 3000
+    check_parity(eng, c, oracle_mod, case, [enc[i % len(enc)][0] for i in range(n)],
+                 [enc[i % len(enc)][2] for i in range(n)])
 
 
 def test_host_end_to_end_and_multi_gpu(eng, ctx, oracle_mod):
@@ -186,13 +295,17 @@ def test_host_end_to_end_and_multi_gpu(eng, ctx, oracle_mod):
     dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     in_ptrs = offs + np.uint64(hin.data_ptr())
     out_ptrs = ooff + np.uint64(hout.data_ptr())
-    st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz_a, batch_bytes=3 * 65536)
-    assert not st.any()
-    res = hout.numpy()
-    for i, o in enumerate(origs):
-        assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
+    for contiguous in (True, False):
+        hout.zero_()
+        st = ctx.unfilter_host(dp, in_ptrs, sizes, out_ptrs, osz_a, batch_bytes=3 * 65536,
+                               contiguous_input=contiguous, contiguous_output=contiguous)
+        assert not st.any()
+        res = hout.numpy()
+        for i, o in enumerate(origs):
+            assert np.array_equal(res[int(ooff[i]):int(ooff[i]) + o.size], o)
     hout.zero_()
-    st = eng.unfilter_multi_gpu(dp, in_ptrs, sizes, out_ptrs, osz_a, [0, 0], batch_bytes=1 << 20)
+    st = eng.unfilter_multi_gpu(dp, in_ptrs, sizes, out_ptrs, osz_a, [0, 0], batch_bytes=1 << 20,
+                                contiguous_input=True, contiguous_output=True)
     assert not st.any()
     res = hout.numpy()
     for i, o in enumerate(origs):
@@ -228,7 +341,8 @@ def test_host_end_to_end_padded_layouts(eng, ctx, oracle_mod):
     hout = torch.full((int(ooff[-1] + osz[-1]) + 32,), 0xAB, dtype=torch.uint8).pin_memory()
     dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     st = ctx.unfilter_host(dp, perm_offs + np.uint64(hin.data_ptr()), sizes,
-                           ooff + np.uint64(hout.data_ptr()), osz, batch_bytes=5 * 65536)
+                           ooff + np.uint64(hout.data_ptr()), osz, batch_bytes=5 * 65536,
+                           contiguous_input=True, contiguous_output=True)
     assert not st.any()
     res = hout.numpy()
     mask = np.ones(res.size, dtype=bool)

@@ -244,7 +244,25 @@ def test_byteshuffle_vs_numpy_transpose(oracle_mod, ts):
 # ---------------------------------------------------------------------------
 # second restatement: workloads.py (numpy) == oracle forward, byte for byte
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", ["ramp", "rand"])
+def test_c5_active_variant_exercises_every_stage():
+    """The 'active' C5 variant: DoubleDelta takes its bit-packed path
+    (bitsize < 8*sizeof(int32) - 1, dd_compressor.cc:233-236) and most BWR
+    windows over DD's output narrow to 8 bits."""
+    import struct
+    import workloads as W
+    rng = np.random.default_rng(3)
+    for t in range(8):
+        v = W.c5_values("active", t, rng)
+        assert W.c5_dd_bitsize(v) < 31
+        f = W.c5_filter_tile(v)
+        ml = struct.unpack_from("<I", f, 16)[0]
+        nw = struct.unpack_from("<I", f, 24)[0]
+        bits = [f[20 + 8 + k * 9 + 4] for k in range(nw)]
+        assert sum(b == 8 for b in bits) > 0.8 * nw
+        assert len(f) < 0.4 * v.nbytes and ml > 0
+
+
+@pytest.mark.parametrize("variant", ["ramp", "rand", "active"])
 def test_numpy_c5_encoder_matches_oracle(oracle_mod, variant):
     import workloads as W
     op = oracle_mod.OraclePipeline(W.c5_pipeline_bytes(), 23, int(Datatype.INT32), 4)

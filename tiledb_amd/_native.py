@@ -50,7 +50,10 @@ SIGNATURES = {
                                                      ctypes.c_uint32, c_i32p,
                                                      ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                                      ctypes.c_uint64]),
+    "tdbg_unfilter_tiles_cpu": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                                               ctypes.c_uint32, c_i32p, ctypes.c_uint32]),
     "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
+    "tdbg_context_path_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "tdbg_context_time_launches": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
     "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint32,

@@ -18,10 +18,14 @@ ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 
 NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART_HOST)
 # (source, object name, extra flags)
-UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_host.cpp", "tdbg_host", [])] +
+UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_host.cpp", "tdbg_host", []),
+          # CPU entry: host-only C++, product and sum rounded separately
+          # (FLOAT_SCALE parity with the reference's x86-64 build)
+          ("tdbg_cpu.cpp", "tdbg_cpu", ["-ffp-contract=off"])] +
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
-HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h"]
+HOST_ONLY = {"tdbg_cpu.cpp"}
+HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h"]
 
 
 def _deps(src: str):
@@ -55,8 +59,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
         objs.append(obj)
         if not force and not _newer(obj, _deps(src)):
             continue
-        cmd = [HIPCC] + (["-x", "hip"] if src.endswith(".cpp") else []) + common + extra + [
-            "-c", os.path.join(CSRC, src), "-o", obj]
+        if src in HOST_ONLY:
+            flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(ROOT, "include")]
+        else:
+            flags = (["-x", "hip"] if src.endswith(".cpp") else []) + common
+        cmd = [HIPCC] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         jobs.append(cmd)
 
     def run(cmd):

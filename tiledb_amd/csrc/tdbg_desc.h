@@ -49,6 +49,21 @@ enum tdbg_fast_kind : uint32_t {
   TDBG_FAST_NONE = 0,
 };
 
+// device path counters (KParams::stats), cumulative per context
+enum tdbg_stat_slot : uint32_t {
+  TDBG_STAT_FUSED_TILES = 0,    // tiles the fused LDS kernel unfiltered (status OK)
+  TDBG_STAT_FUSED_BYTES = 1,    // their unfiltered bytes
+  TDBG_STAT_FALLBACK = 2,       // tiles the fused kernel declined (re-run by the fixup)
+  TDBG_STAT_GENERAL_TILES = 3,  // tiles the general interpreter unfiltered (status OK)
+  TDBG_STAT_GENERAL_BYTES = 4,
+  TDBG_STAT_N = 8
+};
+
+// host-side internals shared by tdbg_host.cpp and tdbg_cpu.cpp
+struct tdbg_pipeline;
+const tdbg_plan* tdbg_internal_plan(const tdbg_pipeline* p);  // null if unsupported
+void tdbg_internal_set_error(const char* msg);                // tdbg_last_error text
+
 namespace tdbg {
 // kernel parameters (passed by value)
 struct KParams {
@@ -66,14 +81,19 @@ struct KParams {
   uint32_t slot_cap, md_cap, tab_cap;
   uint32_t dbg_stop;  // timing-only ablation: stop after N fast stages (0 = off)
   uint32_t fixup;     // general kernel: only the tiles queued in fbq (TDBG_E_FALLBACK)
-  // Fallback queue of this launch: fbq[0] = count, fbq[1 + k] = tile index.
-  // The fused kernel appends the tiles it declines; the fixup launch walks
-  // the queue and clears fbq_next[0], the queue the context's next launch
-  // appends to (two queues alternate per launch on the context's stream).
+  // Fallback queue of this launch: fbq[0] = count, fbq[1 + k] = tile index,
+  // k < fbq_cap (= ntiles: a tile is queued at most once per launch).  The
+  // host zeroes the count on the launch stream right before the fused
+  // kernel, so a queue never carries entries across launches; the fused
+  // kernel appends the tiles it declines, the fixup launch walks the queue.
   uint32_t* fbq;
-  uint32_t* fbq_next;
+  uint32_t fbq_cap;
+  // Device path counters (cumulative per context, TDBG_STAT_*): one atomic
+  // add per workgroup at exit.
+  uint64_t* stats;
   uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
   tdbg_plan plan;
 };
+
 
 }  // namespace tdbg

@@ -146,6 +146,11 @@ __device__ __forceinline__ bool load_to_lds(uint8_t* X, uint32_t cap, const uint
   const uint32_t cnt = (uint32_t)((a1 - a0) >> 4);
   *base = (uint32_t)((uintptr_t)g - a0);
   if (cnt * 16 > cap) return false;
+  // n == 0 at a 16-B aligned g: no unit to load.  (The clamp below would
+  // otherwise read unit cnt - 1 = 2^32 - 1, 64 GiB past g: an empty md or
+  // data section at an aligned address -- reachable once tiles sit back to
+  // back at arbitrary offsets -- faulted the GPU.)
+  if (cnt == 0) return true;
   const g_cu4* src = (const g_cu4*)a0;
   constexpr int LU = (XCAP / 16 + FNT - 1) / FNT;
   // Issue every load first (clamped to a valid unit: no divergent control
@@ -1438,6 +1443,7 @@ unfilter_fused_kernel(const KParams kp) {
   // tiles: all ntiles, or a host-given list (the sync entry's retry)
   const uint64_t ntl = kp.ntiles;
   const uint32_t* tl = kp.tile_list;
+  uint64_t ok_tiles = 0, ok_bytes = 0;
   TileDesc dn{};
   if (blockIdx.x < ntl) {
     dn = desc_uniform(desc_load(kp, tl, blockIdx.x));
@@ -1537,11 +1543,24 @@ unfilter_fused_kernel(const KParams kp) {
     }
     if (!hooked) hook();
     __syncthreads();  // LDS reads of this tile done before the next commit
+    if (rc == TDBG_OK) {
+      ok_tiles++;
+      ok_bytes += os;
+    }
     if (tid_() == 0) {
       if (kp.status) kp.status[t] = rc;
-      if (rc == TDBG_E_FALLBACK && kp.fbq) kp.fbq[1 + atomicAdd(kp.fbq, 1u)] = (uint32_t)t;
+      if (rc == TDBG_E_FALLBACK && kp.fbq) {
+        // bounded: the count was zeroed for this launch and each tile is
+        // queued at most once, so k < fbq_cap always holds
+        const uint32_t k = atomicAdd(kp.fbq, 1u);
+        if (k < kp.fbq_cap) kp.fbq[1 + k] = (uint32_t)t;
+      }
     }
     pc.mark(6);
+  }
+  if (kp.stats && tid_() == 0 && ok_tiles) {
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
   }
   pc.flush();
 }

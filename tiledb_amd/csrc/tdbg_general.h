@@ -350,9 +350,12 @@ __device__ int g_pd(StageIO& io, const tdbg_stage& s, Slot& sl, Shared<NT>& sh) 
 // block-parallel: codes at fixed bit offsets, then x_i from one tuple scan.
 // Returns status; *nvals = values written.
 // ---------------------------------------------------------------------------
+// zero_rest: bytes of the part past the decoded values are zeroed in scratch
+// and left untouched in the tile's fixed allocation (as the oracle models
+// the reference's growable vs preallocated buffers).
 template <int NT>
 __device__ int g_dd_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
-                         uint64_t un, uint32_t w, Shared<NT>& sh) {
+                         uint64_t un, uint32_t w, bool zero_rest, Shared<NT>& sh) {
   if (w == 0) return TDBG_E_DD_TYPE;
   if (cn < 9) return TDBG_E_DATA_READ;
   const uint32_t b = src[0];
@@ -361,16 +364,16 @@ __device__ int g_dd_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
     const uint64_t k = cn - 9;
     if (k > un) return TDBG_E_OUT_FULL;
     g_copy<NT>(dst, src + 9, k);
-    g_zero<NT>(dst + k, un - k);
+    if (zero_rest) g_zero<NT>(dst + k, un - k);
     return TDBG_OK;
   }
   int rc = dd_check(cn, un, w, b, num);
   if (rc) return rc;
   // bytes past the decoded values are unspecified in the reference (realloc'd
-  // memory); zero them for determinism, as the oracle does
+  // memory); zeroed in scratch for determinism, as the oracle does
   {
     const uint64_t nv = num == 0 ? 2 : num;
-    if (nv * w < un) g_zero<NT>(dst + nv * w, un - nv * w);
+    if (zero_rest && nv * w < un) g_zero<NT>(dst + nv * w, un - nv * w);
   }
   const uint64_t x0 = ldn(src + 9, w);
   if (num == 1) {
@@ -422,11 +425,11 @@ __device__ int g_dd_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
 // ---------------------------------------------------------------------------
 template <int NT>
 __device__ int g_rle_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
-                          uint64_t un, uint64_t cs, Slot& sl, Shared<NT>& sh,
+                          uint64_t un, uint64_t cs, bool zero_rest, Slot& sl, Shared<NT>& sh,
                           uint64_t* need) {
   const uint64_t rs = cs + 2;
   const uint64_t nr = cn / rs;
-  if (nr == 0) { g_zero<NT>(dst, un); return TDBG_OK; }
+  if (nr == 0) { if (zero_rest) g_zero<NT>(dst, un); return TDBG_OK; }
   if (cn % rs) return TDBG_E_RLE_FORMAT;
   if ((nr + 1) * 8 > sl.tab_cap) { *need = (nr + 1) * 8 + 64; return TDBG_E_SCRATCH; }
   uint64_t* start = (uint64_t*)sl.tab;
@@ -444,7 +447,7 @@ __device__ int g_rle_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
   const uint64_t total = c;
   __syncthreads();
   if (total * cs > un) return TDBG_E_OUT_FULL;
-  g_zero<NT>(dst + total * cs, un - total * cs);
+  if (zero_rest) g_zero<NT>(dst + total * cs, un - total * cs);
   // contiguous cell range per thread: one binary search, then walk forward
   const uint64_t c0 = total * threadIdx.x / NT, c1 = total * (threadIdx.x + 1) / NT;
   if (c0 < c1) {
@@ -476,7 +479,7 @@ __device__ int g_rle_part(const uint8_t* src, uint64_t cn, uint8_t* dst,
 template <int NT>
 __device__ int g_delta_part(const uint8_t* src, uint64_t cn, uint8_t* dst, uint64_t un,
                             uint32_t w, Shared<NT>& sh) {
-  if (w == 0) return TDBG_E_DD_TYPE;
+  if (w == 0) return TDBG_E_DELTA_TYPE;  // delta_compressor.cc:210-213
   if (cn < 8) return TDBG_E_DATA_READ;
   const uint64_t num = ldn(src, 8);
   const uint64_t nv = num ? num : 1;
@@ -533,9 +536,10 @@ __device__ int g_compression(StageIO& io, const tdbg_stage& s, Slot& sl,
     }
     if (ip + cn > io.in_n) return TDBG_E_DATA_READ;
     int rc;
-    if (s.kind == TDBG_K_DD) rc = g_dd_part<NT>(io.in + ip, cn, dst, un, s.w, sh);
+    const bool zero_rest = is_md || !io.fixed;
+    if (s.kind == TDBG_K_DD) rc = g_dd_part<NT>(io.in + ip, cn, dst, un, s.w, zero_rest, sh);
     else if (s.kind == TDBG_K_DELTA) rc = g_delta_part<NT>(io.in + ip, cn, dst, un, s.w, sh);
-    else rc = g_rle_part<NT>(io.in + ip, cn, dst, un, s.cs, sl, sh, &io.need);
+    else rc = g_rle_part<NT>(io.in + ip, cn, dst, un, s.cs, zero_rest, sl, sh, &io.need);
     __syncthreads();
     if (rc) return rc;
     if (is_md) mo += un; else op += un;

@@ -108,28 +108,47 @@ struct tdbg_pipeline {
   bool supported = true;
 };
 
+// for the CPU entry (tdbg_cpu.cpp): the resolved plan of a supported pipeline
+const tdbg_plan* tdbg_internal_plan(const tdbg_pipeline* p) {
+  return p && p->supported ? &p->plan : nullptr;
+}
+void tdbg_internal_set_error(const char* msg) { g_err = msg; }
+
 struct tdbg_context {
   int device = 0;
   int cus = 256;
-  // general-path scratch
+  // general-path scratch (fixed slot sizes; the sync entry's TDBG_E_SCRATCH
+  // retries use their own buffer, rscratch, so one oversized chunk never
+  // inflates the slots of every later launch)
   uint8_t* scratch = nullptr;
   uint64_t scratch_bytes = 0;
   uint32_t slot_cap = 80 * 1024, md_cap = 16 * 1024, tab_cap = 32 * 1024;
+  uint8_t* rscratch = nullptr;
+  uint64_t rscratch_bytes = 0;
   // per-tile status / need
   int32_t* d_status = nullptr;
   uint64_t* d_need = nullptr;
   uint64_t status_cap = 0;
   uint32_t* d_list = nullptr;
   uint64_t list_cap = 0;
-  // fused-kernel fallback queues (KParams::fbq), alternating per launch
-  uint32_t* d_fbq[2] = {nullptr, nullptr};
-  uint32_t fbq_parity = 0;
+  // fused-kernel fallback queue (KParams::fbq): count + status_cap entries,
+  // count zeroed on the launch stream before every fused launch
+  uint32_t* d_fbq = nullptr;
+  // device path counters (KParams::stats, TDBG_STAT_*)
+  uint64_t* d_stats = nullptr;
+  // Launch ordering: scratch slots, the fallback queue and the status /
+  // need arrays are per context, so a context's launches must not overlap.
+  // Launches on one stream are ordered by the stream; when a launch comes on
+  // a different stream than the previous one, the host first waits for the
+  // previous stream (tdbg_order_stream).
+  hipStream_t last_stream = nullptr;
+  bool last_stream_set = false;
   int64_t last_te = -1;  // tev index of the last armed launch's events
   // armed per-launch timing (tdbg_context_time_launches): event triples
   // {before the fused/general kernel, after it, after the fixup launch}
   std::vector<hipEvent_t> tev;
   uint32_t tcap = 0, tcount = 0;
-  uint64_t tiles_unfiltered = 0, bytes_unfiltered = 0;
+  uint64_t tiles_unfiltered = 0;  // tiles submitted (stats "tiles_unfiltered", reader_base.cc:1074)
   // host E2E staging
   struct Stage {
     uint8_t* d_in = nullptr;
@@ -162,8 +181,17 @@ int ensure_scratch(tdbg_context* c, uint32_t grid) {
   if (need <= c->scratch_bytes) return TDBG_OK;
   if (c->scratch) HIP_OK(hipFree(c->scratch));
   c->scratch = nullptr;
+  c->scratch_bytes = 0;
   HIP_OK(hipMalloc(&c->scratch, need));
   c->scratch_bytes = need;
+  return TDBG_OK;
+}
+
+// Serialize a context's launches across streams (see tdbg_context::last_stream).
+int order_stream(tdbg_context* c, hipStream_t s) {
+  if (c->last_stream_set && c->last_stream != s) HIP_OK(hipStreamSynchronize(c->last_stream));
+  c->last_stream = s;
+  c->last_stream_set = true;
   return TDBG_OK;
 }
 
@@ -171,15 +199,15 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   if (n <= c->status_cap) return TDBG_OK;
   if (c->d_status) HIP_OK(hipFree(c->d_status));
   if (c->d_need) HIP_OK(hipFree(c->d_need));
+  if (c->d_fbq) HIP_OK(hipFree(c->d_fbq));
+  c->d_status = nullptr;
+  c->d_need = nullptr;
+  c->d_fbq = nullptr;
+  c->status_cap = 0;
   HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
   HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
-  for (int k = 0; k < 2; k++) {
-    uint32_t*& q = c->d_fbq[k];
-    if (q) HIP_OK(hipFree(q));
-    q = nullptr;
-    HIP_OK(hipMalloc(&q, (n + 1) * sizeof(uint32_t)));
-    HIP_OK(hipMemset(q, 0, sizeof(uint32_t)));
-  }
+  HIP_OK(hipMalloc(&c->d_fbq, (n + 1) * sizeof(uint32_t)));
+  HIP_OK(hipMemset(c->d_fbq, 0, sizeof(uint32_t)));
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -330,6 +358,7 @@ const char* tdbg_status_str(int s) {
     case TDBG_E_DD_OVERFLOW: return "Cannot compress with DoubleDelta: delta exceeds range of int64_t";
     case TDBG_E_DEVICE: return "HIP runtime error";
     case TDBG_E_DESCRIPTOR: return "Deserialization error; malformed filter pipeline";
+    case TDBG_E_DELTA_TYPE: return "Decompression is not yet supported for float datatypes.";
     default: return "unknown";
   }
 }
@@ -449,6 +478,13 @@ int tdbg_context_create(int device, tdbg_context** out) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
     c->cus = cus;
+  hipError_t e = hipMalloc(&c->d_stats, sizeof(uint64_t) * TDBG_STAT_N);
+  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, sizeof(uint64_t) * TDBG_STAT_N);
+  if (e != hipSuccess) {
+    if (c->d_stats) (void)hipFree(c->d_stats);
+    delete c;
+    return fail(TDBG_E_DEVICE, std::string("tdbg_context_create: ") + hipGetErrorString(e));
+  }
   *out = c;
   return TDBG_OK;
 }
@@ -461,8 +497,9 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->d_need) (void)hipFree(c->d_need);
   if (c->d_list) (void)hipFree(c->d_list);
-  for (auto* q : c->d_fbq)
-    if (q) (void)hipFree(q);
+  if (c->d_fbq) (void)hipFree(c->d_fbq);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->rscratch) (void)hipFree(c->rscratch);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -535,12 +572,15 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       kp.prof = c->d_prof;
     }
   }
+  kp.stats = c->d_stats;
   const bool queued = fast && d_status && !kp.dbg_stop;
   if (queued) {
-    kp.fbq = c->d_fbq[c->fbq_parity];
-    kp.fbq_next = c->d_fbq[c->fbq_parity ^ 1];
-    c->fbq_parity ^= 1;
+    if (ntiles > c->status_cap) return fail(TDBG_E_ARG, "internal: fallback queue smaller than the launch");
+    kp.fbq = c->d_fbq;
+    kp.fbq_cap = (uint32_t)ntiles;
   }
+  // the queue starts empty for this launch, whatever ran before on any stream
+  if (queued) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   // Events only on armed launches (tdbg_context_time_launches): an event
   // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
@@ -577,7 +617,9 @@ int tdbg_unfilter_tiles_async(tdbg_context* c, const tdbg_pipeline* p, uint64_t 
     return fail(TDBG_E_ARG, "null tile arrays");
   if (ntiles > 0xffffffffull) return fail(TDBG_E_ARG, "too many tiles in one call");
   HIP_OK(hipSetDevice(c->device));
-  int rc = ensure_status(c, ntiles);
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  rc = ensure_status(c, ntiles);
   if (rc) return rc;
   rc = launch(c, p, ntiles, d_in, d_in_size, d_out, d_out_size, flags,
               d_status ? d_status : c->d_status, c->d_need, nullptr, (hipStream_t)stream, false);
@@ -597,7 +639,9 @@ int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   if (ntiles > 0xffffffffull) return fail(TDBG_E_ARG, "too many tiles in one call");
   HIP_OK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
-  int rc = ensure_status(c, ntiles);
+  int rc = order_stream(c, s);
+  if (rc) return rc;
+  rc = ensure_status(c, ntiles);
   if (rc) return rc;
   rc = launch(c, p, ntiles, d_in, d_in_size, d_out, d_out_size, flags, c->d_status, c->d_need,
               nullptr, s, false);
@@ -615,33 +659,40 @@ int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     for (uint64_t i = 0; i < ntiles; i++)
       if (st[i] == TDBG_E_SCRATCH) { list.push_back((uint32_t)i); maxneed = std::max(maxneed, need[i]); }
     if (list.empty()) break;
-    const uint64_t grow = std::max<uint64_t>(maxneed + maxneed / 4 + 256, 0);
+    // retry-only slot sizes (the context's own slots keep their defaults):
+    // the cap that was short is not known, so all three grow to the need
+    const uint64_t grow = (std::max<uint64_t>(maxneed + maxneed / 4 + 256, 0) + 255) & ~255ull;
     if (grow > 0xffffffffull / 2) return fail(TDBG_E_SCRATCH, "chunk stage larger than 2 GiB");
-    c->slot_cap = (uint32_t)std::max<uint64_t>(c->slot_cap, (grow + 255) & ~255ull);
-    c->md_cap = (uint32_t)std::max<uint64_t>(c->md_cap, (grow + 255) & ~255ull);
-    c->tab_cap = (uint32_t)std::max<uint64_t>(c->tab_cap, (grow + 255) & ~255ull);
+    const uint32_t rslot = (uint32_t)std::max<uint64_t>(c->slot_cap, grow);
+    const uint32_t rmd = (uint32_t)std::max<uint64_t>(c->md_cap, grow);
+    const uint32_t rtab = (uint32_t)std::max<uint64_t>(c->tab_cap, grow);
+    const uint64_t rslot_bytes = 2ull * rslot + 2ull * rmd + rtab;
     if (list.size() > c->list_cap) {
       if (c->d_list) HIP_OK(hipFree(c->d_list));
+      c->d_list = nullptr;
+      c->list_cap = 0;
       HIP_OK(hipMalloc(&c->d_list, list.size() * 4));
       c->list_cap = list.size();
     }
     HIP_OK(hipMemcpyAsync(c->d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(list.size(), 256);
-    // shrink scratch for the retry: fewer, bigger slots
-    if (c->scratch && slot_bytes(c) * grid > c->scratch_bytes) {
+    // few, big slots: at most 256 MiB of retry scratch (at least one slot)
+    const uint64_t by_mem = std::max<uint64_t>(1, (256ull << 20) / rslot_bytes);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(list.size(), 64), by_mem);
+    if (rslot_bytes * grid > c->rscratch_bytes) {
       HIP_OK(hipStreamSynchronize(s));
-      HIP_OK(hipFree(c->scratch));
-      c->scratch = nullptr;
-      c->scratch_bytes = 0;
+      if (c->rscratch) HIP_OK(hipFree(c->rscratch));
+      c->rscratch = nullptr;
+      c->rscratch_bytes = 0;
+      HIP_OK(hipMalloc(&c->rscratch, rslot_bytes * grid));
+      c->rscratch_bytes = rslot_bytes * grid;
     }
-    rc = ensure_scratch(c, grid);
-    if (rc) return rc;
     tdbg::KParams kp{};
     kp.in = d_in; kp.in_size = d_in_size; kp.out = d_out; kp.out_size = d_out_size;
     kp.status = c->d_status; kp.need = c->d_need; kp.tile_list = c->d_list;
     kp.ntiles = list.size(); kp.flags = flags; kp.plan = p->plan;
-    kp.scratch = c->scratch; kp.slot_bytes = slot_bytes(c);
-    kp.slot_cap = c->slot_cap; kp.md_cap = c->md_cap; kp.tab_cap = c->tab_cap;
+    kp.scratch = c->rscratch; kp.slot_bytes = rslot_bytes;
+    kp.slot_cap = rslot; kp.md_cap = rmd; kp.tab_cap = rtab;
+    kp.stats = c->d_stats;
     hipError_t e = tdbg_launch_general(&kp, grid, s);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("retry launch: ") + hipGetErrorString(e));
     HIP_OK(hipMemcpyAsync(st.data(), c->d_status, ntiles * 4, hipMemcpyDeviceToHost, s));
@@ -659,10 +710,32 @@ int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   return TDBG_OK;
 }
 
+static int read_stats(const tdbg_context* c, uint64_t (&h)[TDBG_STAT_N]) {
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  return TDBG_OK;
+}
+
 int tdbg_context_stats(const tdbg_context* c, uint64_t* tiles, uint64_t* bytes) {
   if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
   if (tiles) *tiles = c->tiles_unfiltered;
-  if (bytes) *bytes = c->bytes_unfiltered;
+  if (bytes) *bytes = h[TDBG_STAT_FUSED_BYTES] + h[TDBG_STAT_GENERAL_BYTES];
+  return TDBG_OK;
+}
+
+int tdbg_context_path_stats(const tdbg_context* c, uint64_t* fused_tiles, uint64_t* fallback_tiles,
+                            uint64_t* general_tiles) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (fused_tiles) *fused_tiles = h[TDBG_STAT_FUSED_TILES];
+  if (fallback_tiles) *fallback_tiles = h[TDBG_STAT_FALLBACK];
+  if (general_tiles) *general_tiles = h[TDBG_STAT_GENERAL_TILES];
   return TDBG_OK;
 }
 
@@ -759,17 +832,21 @@ static int stage_reserve(tdbg_context::Stage& s, uint64_t in_b, uint64_t out_b, 
 // tiles join only when exactly contiguous: padding must never be overwritten.
 static constexpr uint64_t kInGap = 64;
 
-static bool in_joins(const uint8_t* const* host, const uint64_t* size, uint64_t j) {
+// Only with TDBG_HOST_CONTIGUOUS_INPUT: without it, two tiles adjacent in
+// the address space may sit in different allocations (e.g. two pinned
+// blocks), and one copy must not span allocations.
+static bool in_joins(const uint8_t* const* host, const uint64_t* size, uint64_t j, bool coalesce) {
+  if (!coalesce) return false;
   const uint8_t* end = host[j - 1] + size[j - 1];
   return host[j] >= end && (uint64_t)(host[j] - end) <= kInGap;
 }
 
 // device offsets (relative to the stage's d_in) of tiles [lo, hi); returns the span
 static uint64_t in_dev_offsets(const uint8_t* const* host, const uint64_t* size, uint64_t lo,
-                               uint64_t hi, uint64_t* off) {
+                               uint64_t hi, uint64_t* off, bool coalesce) {
   uint64_t o = 0;
   for (uint64_t i = lo; i < hi; i++) {
-    if (i > lo && in_joins(host, size, i)) o += (uint64_t)(host[i] - (host[i - 1] + size[i - 1]));
+    if (i > lo && in_joins(host, size, i, coalesce)) o += (uint64_t)(host[i] - (host[i - 1] + size[i - 1]));
     if (off) off[i - lo] = o;
     o += size[i];
   }
@@ -778,19 +855,19 @@ static uint64_t in_dev_offsets(const uint8_t* const* host, const uint64_t* size,
 
 static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* const* host,
                        const uint64_t* size, uint8_t* dev_base, bool h2d,
-                       uint8_t* const* host_out) {
+                       uint8_t* const* host_out, bool coalesce) {
   uint64_t i = lo;
   uint64_t doff = 0;
   while (i < hi) {
     uint64_t j = i + 1;
     uint64_t bytes = size[i];
     if (h2d) {
-      while (j < hi && in_joins(host, size, j)) { bytes = (uint64_t)(host[j] + size[j] - host[i]); j++; }
+      while (j < hi && in_joins(host, size, j, coalesce)) { bytes = (uint64_t)(host[j] + size[j] - host[i]); j++; }
       if (bytes) HIP_OK(hipMemcpyAsync(dev_base + doff, host[i], bytes, hipMemcpyHostToDevice, st));
       doff += bytes;
       // the next span starts where in_dev_offsets puts it: right after this one
     } else {
-      while (j < hi && host_out[j] == host_out[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
+      while (coalesce && j < hi && host_out[j] == host_out[j - 1] + size[j - 1]) { bytes += size[j]; j++; }
       if (bytes) HIP_OK(hipMemcpyAsync(host_out[i], dev_base + doff, bytes, hipMemcpyDeviceToHost, st));
       doff += bytes;
     }
@@ -809,9 +886,16 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   if (!in || !in_size || !out || !out_size) return fail(TDBG_E_ARG, "null tile arrays");
   HIP_OK(hipSetDevice(c->device));
   if (batch_bytes == 0) batch_bytes = 256ull << 20;
+  const bool cin = (flags & TDBG_HOST_CONTIGUOUS_INPUT) != 0;
+  const bool cout = (flags & TDBG_HOST_CONTIGUOUS_OUTPUT) != 0;
+  flags &= ~(TDBG_HOST_CONTIGUOUS_INPUT | TDBG_HOST_CONTIGUOUS_OUTPUT);
   if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
   if (!c->hstream) HIP_OK(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
   if (!c->dstream) HIP_OK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+  {
+    int rc = order_stream(c, c->cstream);
+    if (rc) return rc;
+  }
   // batches bounded by bytes on both sides
   std::vector<uint64_t> cuts{0};
   uint64_t bi = 0, bo = 0;
@@ -845,7 +929,7 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     const uint64_t lo = cuts[b], hi = cuts[b + 1], nt = hi - lo;
     uint64_t ob = 0;
     for (uint64_t i = lo; i < hi; i++) ob += out_size[i];
-    const uint64_t ib = in_dev_offsets(in, in_size, lo, hi, nullptr);
+    const uint64_t ib = in_dev_offsets(in, in_size, lo, hi, nullptr, cin);
     int rc = stage_reserve(S, ib + 16, ob + 16, nt);
     if (rc) return rc;
     // pointer/size arrays (pinned) -> device
@@ -853,7 +937,7 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     uint64_t* hs = (uint64_t*)(hp + nt);
     uint8_t** ho = (uint8_t**)(hs + nt);
     uint64_t* hos = (uint64_t*)(ho + nt);
-    in_dev_offsets(in, in_size, lo, hi, (uint64_t*)hp);  // offsets first, pointers below
+    in_dev_offsets(in, in_size, lo, hi, (uint64_t*)hp, cin);  // offsets first, pointers below
     uint64_t oo = 0;
     for (uint64_t i = lo; i < hi; i++) {
       hp[i - lo] = S.d_in + (uint64_t)(uintptr_t)hp[i - lo];
@@ -863,7 +947,7 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
       oo += out_size[i];
     }
     HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, c->hstream));
-    rc = copy_ranges(c->hstream, lo, hi, in, in_size, S.d_in, true, nullptr);
+    rc = copy_ranges(c->hstream, lo, hi, in, in_size, S.d_in, true, nullptr, cin);
     if (rc) return rc;
     const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
     const uint64_t* ds = (const uint64_t*)(dp + nt);
@@ -879,7 +963,7 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     HIP_OK(hipEventRecord(S.kdone, c->cstream));
     HIP_OK(hipStreamWaitEvent(c->dstream, S.kdone, 0));
     HIP_OK(hipMemcpyAsync(S.h_status, S.d_stat, nt * 4, hipMemcpyDeviceToHost, c->dstream));
-    rc = copy_ranges(c->dstream, lo, hi, nullptr, out_size, S.d_out, false, out);
+    rc = copy_ranges(c->dstream, lo, hi, nullptr, out_size, S.d_out, false, out, cout);
     if (rc) return rc;
     HIP_OK(hipEventRecord(S.done, c->dstream));
     pending[k] = true;

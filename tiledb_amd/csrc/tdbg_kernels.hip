@@ -39,17 +39,27 @@ __device__ __attribute__((noinline)) void general_body(const KParams& kp) {
   const uint32_t* list = kp.tile_list;
   if (kp.fixup) {  // only the tiles the fused kernel queued
     n = kp.fbq[0];
+    if (n > kp.fbq_cap) n = kp.fbq_cap;
     list = kp.fbq + 1;
   }
+  uint64_t ok_tiles = 0, ok_bytes = 0;
   for (uint64_t j = blockIdx.x; j < n; j += gridDim.x) {
     const uint64_t t = list ? list[j] : j;
     uint64_t need = 0;
     const int rc = g_tile<GEN_NT>(kp, kp.in[t], kp.in_size[t], kp.out[t], kp.out_size[t], sl, sh, &need);
     __syncthreads();
+    if (rc == TDBG_OK) {
+      ok_tiles++;
+      ok_bytes += kp.out_size[t];
+    }
     if (threadIdx.x == 0) {
       if (kp.status) kp.status[t] = rc;
       if (kp.need) kp.need[t] = need;
     }
+  }
+  if (kp.stats && threadIdx.x == 0 && ok_tiles) {
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_GENERAL_TILES], (unsigned long long)ok_tiles);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_GENERAL_BYTES], (unsigned long long)ok_bytes);
   }
 }
 
@@ -64,8 +74,10 @@ unfilter_general_kernel(const KParams kp) {
 __global__ void __launch_bounds__(GEN_NT)
 unfilter_fixup_kernel(const KParams kp) {
   const uint32_t queued = kp.fbq[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) kp.fbq_next[0] = 0;
   if (queued == 0) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && kp.stats)
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FALLBACK],
+              (unsigned long long)(queued < kp.fbq_cap ? queued : kp.fbq_cap));
   const KParams local = kp;  // copied only past the early exit
   general_body(local);
 }

@@ -15,6 +15,8 @@ from . import _native
 from ._native import lib
 
 TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
+HOST_CONTIGUOUS_INPUT = 0x2   # TDBG_HOST_CONTIGUOUS_INPUT
+HOST_CONTIGUOUS_OUTPUT = 0x4  # TDBG_HOST_CONTIGUOUS_OUTPUT
 
 
 class EngineError(RuntimeError):
@@ -62,6 +64,17 @@ class DevicePipeline:
         if h:
             lib.tdbg_pipeline_destroy(h)
             self.h = None
+
+
+def pack_offsets(sizes: np.ndarray, align: int = 1) -> np.ndarray:
+    """Start offsets of tiles packed in order, each start rounded up to `align`."""
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    a = np.uint64(max(1, int(align)))
+    al = (sizes + a - np.uint64(1)) // a * a
+    offs = np.zeros_like(sizes)
+    if sizes.size:
+        offs[1:] = np.cumsum(al)[:-1]
+    return offs
 
 
 class TileBatch:
@@ -116,16 +129,17 @@ class TileBatch:
         return cls(d_in, in_off, in_size, d_out, out_off, out_size)
 
     @classmethod
-    def from_host(cls, tiles: Sequence, out_sizes, device: int = 0, fill: int = 0) -> "TileBatch":
+    def from_host(cls, tiles: Sequence, out_sizes, device: int = 0, fill: int = 0,
+                  align: int = 1) -> "TileBatch":
+        """Packs the filtered tiles into one device buffer.  align=1 (default)
+        packs them back to back, as a fragment file holds them and as
+        FilteredData::data_at hands them over (filtered_data.h:100-101: tile
+        starts at cumulative filtered sizes, i.e. arbitrary byte offsets)."""
         bufs = [np.frombuffer(bytes(t), dtype=np.uint8) if not isinstance(t, np.ndarray)
                 else np.ascontiguousarray(t).view(np.uint8).reshape(-1) for t in tiles]
         sizes = np.array([b.size for b in bufs], dtype=np.uint64)
-        # 16-byte aligned packing keeps every tile start aligned like a VFS read
-        al = (sizes + np.uint64(15)) // np.uint64(16) * np.uint64(16)
-        offs = np.zeros_like(sizes)
-        if sizes.size:
-            offs[1:] = np.cumsum(al)[:-1]
-        packed = np.zeros(int(al.sum()) if al.size else 0, dtype=np.uint8)
+        offs = pack_offsets(sizes, align)
+        packed = np.zeros(int(offs[-1] + sizes[-1]) if sizes.size else 0, dtype=np.uint8)
         for b, o in zip(bufs, offs):
             packed[int(o):int(o) + b.size] = b
         return cls.from_packed(packed, offs, sizes, out_sizes, device=device, fill=fill)
@@ -181,6 +195,19 @@ class Context:
             TILE_OFFSETS if offsets_tiles else 0, batch.d_status.data_ptr(),
             self._stream(stream)), "tdbg_unfilter_tiles_async")
 
+    def path_stats(self):
+        """(fused, fallback, general) tile counts, cumulative (synchronizes the device)."""
+        f, b, g = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.tdbg_context_path_stats(self.h, ctypes.byref(f), ctypes.byref(b), ctypes.byref(g)),
+               "tdbg_context_path_stats")
+        return int(f.value), int(b.value), int(g.value)
+
+    def stats(self):
+        """(tiles_unfiltered, read_unfiltered_byte_num)."""
+        t, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.tdbg_context_stats(self.h, ctypes.byref(t), ctypes.byref(b)), "tdbg_context_stats")
+        return int(t.value), int(b.value)
+
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()
         _check(lib.tdbg_context_last_kernel_ms(self.h, ctypes.byref(ms)), "last_kernel_ms")
@@ -210,8 +237,11 @@ class Context:
 
     def unfilter_host(self, dp: DevicePipeline, in_ptrs: np.ndarray, in_size: np.ndarray,
                       out_ptrs: np.ndarray, out_size: np.ndarray, offsets_tiles: bool = False,
-                      batch_bytes: int = 0) -> np.ndarray:
-        """Host-resident end-to-end (pinned H2D, unfilter, D2H)."""
+                      batch_bytes: int = 0, contiguous_input: bool = False,
+                      contiguous_output: bool = False) -> np.ndarray:
+        """Host-resident end-to-end (pinned H2D, unfilter, D2H).  contiguous_*:
+        the caller states that all input (output) buffers lie in one host
+        allocation, which lets adjacent tiles share one copy."""
         n = int(in_size.size)
         st = np.zeros(max(n, 1), dtype=np.int32)
         ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
@@ -220,15 +250,39 @@ class Context:
         osz = np.ascontiguousarray(out_size, dtype=np.uint64)
         rc = lib.tdbg_unfilter_tiles_host(
             self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data, osz.ctypes.data,
-            TILE_OFFSETS if offsets_tiles else 0,
+            _host_flags(offsets_tiles, contiguous_input, contiguous_output),
             st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), batch_bytes)
         if rc and not st[:n].any():
             _check(rc, "tdbg_unfilter_tiles_host")
         return st[:n]
 
 
+def unfilter_cpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, nthreads: int = 0,
+                 offsets_tiles: bool = False) -> np.ndarray:
+    """tdbg_unfilter_tiles_cpu: host tiles -> host outputs on nthreads host
+    threads (0 = hardware concurrency); returns per-tile statuses."""
+    n = int(np.asarray(in_size).size)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
+    isz = np.ascontiguousarray(in_size, dtype=np.uint64)
+    op = np.ascontiguousarray(out_ptrs, dtype=np.uint64)
+    osz = np.ascontiguousarray(out_size, dtype=np.uint64)
+    rc = lib.tdbg_unfilter_tiles_cpu(dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data,
+                                     osz.ctypes.data, TILE_OFFSETS if offsets_tiles else 0,
+                                     st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
+    if rc and not st[:n].any():
+        _check(rc, "tdbg_unfilter_tiles_cpu")
+    return st[:n]
+
+
+def _host_flags(offsets_tiles: bool, contiguous_input: bool, contiguous_output: bool) -> int:
+    return ((TILE_OFFSETS if offsets_tiles else 0) | (HOST_CONTIGUOUS_INPUT if contiguous_input else 0) |
+            (HOST_CONTIGUOUS_OUTPUT if contiguous_output else 0))
+
+
 def unfilter_multi_gpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, devices,
-                       offsets_tiles: bool = False, batch_bytes: int = 0) -> np.ndarray:
+                       offsets_tiles: bool = False, batch_bytes: int = 0,
+                       contiguous_input: bool = False, contiguous_output: bool = False) -> np.ndarray:
     n = int(np.asarray(in_size).size)
     st = np.zeros(max(n, 1), dtype=np.int32)
     ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
@@ -238,8 +292,8 @@ def unfilter_multi_gpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size,
     devs = (ctypes.c_int * len(devices))(*devices)
     rc = lib.tdbg_unfilter_tiles_multi_gpu(
         dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data, osz.ctypes.data,
-        TILE_OFFSETS if offsets_tiles else 0, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-        devs, len(devices), batch_bytes)
+        _host_flags(offsets_tiles, contiguous_input, contiguous_output),
+        st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), devs, len(devices), batch_bytes)
     if rc and not st[:n].any():
         _check(rc, "tdbg_unfilter_tiles_multi_gpu")
     return st[:n]

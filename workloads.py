@@ -352,11 +352,35 @@ def pool(name: str, variant: str, nunique: int, seed: int):
 
 
 def c5_values(variant: str, tile_index: int, rng: np.random.Generator) -> np.ndarray:
+    """C5 tile values.
+    rand:   uniform int32; every byte moves, DD falls back to raw and every BWR
+            window is raw (two stages are views).
+    ramp:   a = tile*16384 + i; DD raw (bitsize 33 >= 31), half the BWR windows
+            8-bit.
+    active: a low-cardinality step column (runs of U{256..2047} equal values,
+            values U{0..15}): all three stages do work -- DoubleDelta bitsize 28
+            (< 31: the bit-packed path), ~92 % of the BWR windows over DD's
+            output 8-bit, byteshuffle over the whole tile (~20 KB filtered)."""
     if variant == "ramp":
         return (np.arange(TILE_VALUES, dtype=np.int64) + tile_index * TILE_VALUES).astype(np.int32)
     if variant == "rand":
         return rng.integers(-2**31, 2**31, TILE_VALUES, dtype=np.int64).astype(np.int32)
+    if variant == "active":
+        out = np.empty(TILE_VALUES, dtype=np.int32)
+        i = 0
+        while i < TILE_VALUES:
+            n = int(rng.integers(256, 2048))
+            out[i:i + n] = rng.integers(0, 16)
+            i += n
+        return out
     raise ValueError(variant)
+
+
+def c5_dd_bitsize(values: np.ndarray) -> int:
+    """DoubleDelta bitsize of a C5 tile's data part (after the byteshuffle)."""
+    raw = np.ascontiguousarray(values, dtype="<i4")
+    shuf = raw.view(np.uint8).reshape(-1, 4).T.reshape(-1)
+    return _dd_int32(shuf.view("<i4"))[0]
 
 
 def c5_pool(variant: str, nunique: int, seed: int = 5) -> Tuple[List[bytes], List[np.ndarray]]:
