@@ -574,7 +574,51 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     const uint32_t w = pow2 ? (o >> wsh) : (o / ws0);
     return w < nw ? w : nw - 1;
   };
-  if ((W == 4 || W == 8) && ws0 % 16 == 0) {
+  if (W == 4 && ws0 % 16 == 0) {
+    // 32-bit values: compressed widths are 8 or 16 bits (32 is raw), so a
+    // 16-B output unit = 4 elements from <= 8 source bytes (q0, q1) with
+    // 32-bit bit-field extracts; raw units take the 16 bytes as they are.
+    auto fn16w4 = [&](uint32_t u, uint32_t (&wv)[4]) {
+      const uint32_t o = 16 * u, w = win(o);
+      const uint4 e = L.TAB[w];
+      const uint32_t ob = o - w * ws0;
+      const bool raw = (e.y & 0x100u) != 0;
+      const uint32_t bits = e.y & 0xf8u;  // 8 * compressed bytes
+      const uint32_t src = base + e.x + (raw ? ob : (ob >> 2) * (bits >> 3));
+      const uint32_t a = src & ~3u, sh = src & 3u;
+      uint32_t d[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) d[k] = *(const uint32_t*)(X + a + 4 * k);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      const uint64_t Q = ((uint64_t)q[1] << 32) | q[0];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t lo = k == 0 ? q[0] : (uint32_t)(Q >> (k * bits));
+        const uint32_t v = SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)lo, 0, bits)
+                               : __builtin_amdgcn_ubfe(lo, 0, bits);
+        wv[k] = raw ? q[k] : v + e.z;
+      }
+    };
+    drive2<16>(L, orig, orig / 16, final, gout, fn16w4, [&](uint32_t u, uint32_t (&wv)[4]) {
+      // partial last unit: element-wise (the window may hold fewer bytes)
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t o = 16 * u + 4 * k;
+        const uint32_t w = win(o);
+        const uint4 e = L.TAB[w];
+        const uint32_t ob = o - w * ws0;
+        uint64_t v = 0;
+        if (o < orig) {
+          if (e.y & 0x100u) v = ldsn(X, base + e.x + ob, 4);
+          else v = bwr_elem<W, SGN>(X, base, e, ob / 4);
+        }
+        wv[k] = (uint32_t)v;
+      }
+    });
+  } else if ((W == 4 || W == 8) && ws0 % 16 == 0) {
     // Every 16-B output unit lies in one window: one TAB read per unit, the
     // unit's source bytes read as one aligned span, elements extracted in
     // registers.  Compressed elements of a unit span at most 8 bytes.
@@ -696,33 +740,6 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
 // ---------------------------------------------------------------------------
 // scans with a per-thread element count
 // ---------------------------------------------------------------------------
-// Double-delta tuple (E, X) exclusive scan; cnt elements per thread.
-__device__ __forceinline__ void block_ddscan_n(uint64_t& E, uint64_t& Xs, uint64_t cnt,
-                                               uint64_t* red) {
-  const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
-  uint64_t iE = E, iX = Xs;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t oE = __shfl_up(iE, d, 64), oX = __shfl_up(iX, d, 64);
-    if (lane >= (uint32_t)d) {
-      iX = oX + iX + (uint64_t)d * cnt * oE;
-      iE = oE + iE;
-    }
-  }
-  uint64_t eE = __shfl_up(iE, 1, 64), eX = __shfl_up(iX, 1, 64);
-  if (lane == 0) { eE = 0; eX = 0; }
-  if (lane == 63) { red[2 * wid] = iE; red[2 * wid + 1] = iX; }
-  __syncthreads();
-  uint64_t PE = 0, PX = 0;
-  for (uint32_t i = 0; i < wid; i++) {
-    PX = PX + red[2 * i + 1] + 64ull * cnt * PE;
-    PE += red[2 * i];
-  }
-  __syncthreads();
-  E = PE + eE;
-  Xs = PX + eX + (uint64_t)lane * cnt * PE;
-}
-
 // Segmented sum (positive delta windows): aggregate (has_head, sum after the
 // last head).  Exclusive scan; returns the carry into this thread's slice.
 __device__ __forceinline__ uint64_t block_segscan(bool has, uint64_t sum, uint64_t* red) {
@@ -940,114 +957,267 @@ __device__ bool rle_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32
 // ---------------------------------------------------------------------------
 // DD data part (block-parallel, in place)
 // ---------------------------------------------------------------------------
-// MSB-first 32-bit chunk c of the u64 word stream at byte offset bs
-__device__ __forceinline__ uint32_t dd_chunk(const uint8_t* X, uint32_t bs, uint32_t c) {
-  const uint32_t off = bs + 8 * (c >> 1) + ((c & 1) ? 0u : 4u);
-  return lds32(X, off < XCAP + MDCAP - 8 ? off : 0);
+// Double-delta tuple (E, X) exclusive scan in the value width's arithmetic
+// (U = uint32_t for W <= 4: everything is modulo 2^(8W) anyway); cnt
+// elements per thread.
+template <class U>
+__device__ __forceinline__ void block_ddscan_u(U& E, U& Xs, uint32_t cnt, U* red) {
+  const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
+  U iE = E, iX = Xs;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const U oE = __shfl_up(iE, d, 64), oX = __shfl_up(iX, d, 64);
+    if (lane >= (uint32_t)d) {
+      iX = oX + iX + (U)d * (U)cnt * oE;
+      iE = oE + iE;
+    }
+  }
+  U eE = __shfl_up(iE, 1, 64), eX = __shfl_up(iX, 1, 64);
+  if (lane == 0) { eE = 0; eX = 0; }
+  if (lane == 63) { red[2 * wid] = iE; red[2 * wid + 1] = iX; }
+  __syncthreads();
+  U PE = 0, PX = 0;
+#pragma unroll
+  for (int i = 0; i < FNT / 64; i++) {
+    if ((uint32_t)i < wid) {
+      PX = PX + red[2 * i + 1] + (U)64 * (U)cnt * PE;
+      PE += red[2 * i];
+    }
+  }
+  __syncthreads();
+  E = PE + eE;
+  Xs = PX + eX + (U)lane * (U)cnt * PE;
 }
 
-// Sequential MSB-first code reader over a thread's contiguous codes.
-struct DDReader {
-  const uint8_t* X;
-  uint32_t bs, c, w0, w1, w2;
-  uint64_t s;
-  __device__ __forceinline__ void init(const uint8_t* X_, uint32_t bs_, uint64_t s_) {
-    X = X_; bs = bs_; s = s_;
-    c = (uint32_t)(s >> 5);
-    w0 = dd_chunk(X, bs, c);
-    w1 = dd_chunk(X, bs, c + 1);
-    w2 = dd_chunk(X, bs, c + 2);
-  }
-  // next code of cb = b + 1 bits, as a signed difference modulo 2^64.
-  // NARROW: cb <= 32 (W <= 4), so the window advances by at most one chunk.
-  template <bool NARROW>
-  __device__ __forceinline__ uint64_t next(uint32_t b) {
-    const uint32_t cc = (uint32_t)(s >> 5);
-    if (NARROW) {
-      if (c < cc) { w0 = w1; w1 = w2; w2 = dd_chunk(X, bs, c + 3); c++; }
-    } else {
-      while (c < cc) { w0 = w1; w1 = w2; w2 = dd_chunk(X, bs, c + 3); c++; }
-    }
-    const uint32_t sh = (uint32_t)(s & 31);
-    s += b + 1;
-    if (NARROW) {
-      // top 32 bits of the window starting at bit sh
-      const uint32_t top = sh ? __builtin_amdgcn_alignbit(w0, w1, 32 - sh) : w0;
-      const uint32_t code = top >> (31 - b);
-      const uint32_t mag = b ? (code & ((1u << b) - 1)) : 0;
-      return ((code >> b) & 1) ? (0 - (uint64_t)mag) : (uint64_t)mag;
-    }
-    uint64_t top = (((uint64_t)w0 << 32) | w1) << sh;
-    if (sh) top |= (uint64_t)w2 >> (32 - sh);
-    const uint64_t code = top >> (63 - b);
-    const uint64_t mag = b ? (code & ((1ull << b) - 1)) : 0;
-    return ((code >> b) & 1) ? (0 - mag) : mag;
-  }
-};
+// LDS byte offset of MSB-first 32-bit chunk c of the u64 word stream at bs
+// (word c/2 little-endian: its high dword is chunk 2k, its low dword 2k+1)
+__device__ __forceinline__ uint32_t dd_chunk_off(uint32_t bs, uint32_t c) {
+  return bs + 8 * (c >> 1) + ((c & 1) ? 0u : 4u);
+}
 
 // DoubleDelta data part, block-parallel, in place: x_i from the tuple scan of
 // the codes.  Arithmetic is modulo 2^(8W) (32-bit lanes for W <= 4), which is
 // exactly the reference's (T)(dd + 2*x[i-1] - x[i-2]) (dd_compressor.cc:355).
-template <int W>
-__device__ __forceinline__ void dd_decode_part(FastLds& L, uint32_t src, uint32_t b,
-                                                          uint64_t num) {
+// Each thread owns EP = SP / W consecutive values: it decodes their codes
+// once into registers (independent chunk reads in groups of DG), scans the
+// (E, X) tuple over the workgroup, then emits x from the registers.
+template <int W, bool ALIGNED, class M>
+__device__ __forceinline__ void dd_decode_part_t(FastLds& L, uint32_t src, uint32_t b, uint32_t num,
+                                                 M&& mark) {
   typedef typename std::conditional<(W == 8), uint64_t, uint32_t>::type U;
-  constexpr int EP = SP / W;
+  constexpr int EP = SP / W;   // 32 (W = 4) or 16 (W = 8) values per thread
+  constexpr int DG = 4;        // codes per group of in-flight LDS reads
+  constexpr int NC = W == 8 ? 3 : 2;  // chunks per code window
   const uint8_t* X = L.X;
   const U x0 = (U)ldsn(X, src + 9, W), x1 = (U)ldsn(X, src + 9 + W, W);
   const uint32_t bs = src + 9 + 2 * W;
   const U dinit = x1 - x0, xinit = x0 - dinit;
+  const uint32_t cb = b + 1;
   const uint32_t i0 = tid_() * EP;
-  const uint32_t first = i0 < 2 ? 2 : i0;
-  const uint64_t s0 = (uint64_t)(first - 2) * (b + 1);
-  // pass 1: aggregates only
+  const uint32_t lim = XCAP - 8;  // clamp for the (masked) reads of absent codes
+  U e[EP];
+#pragma unroll
+  for (int g = 0; g < EP; g += DG) {
+    uint32_t ch[DG][NC];
+#pragma unroll
+    for (int q = 0; q < DG; q++) {
+      const uint32_t i = i0 + g + q;
+      const uint32_t s = (i >= 2 ? i - 2 : 0) * cb;
+      const uint32_t c = s >> 5;
+#pragma unroll
+      for (int h = 0; h < NC; h++) {
+        uint32_t off = dd_chunk_off(bs, c + h);
+        off = off < lim ? off : 0;
+        ch[q][h] = ALIGNED ? *(const uint32_t*)(X + off) : lds32(X, off);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < DG; q++) {
+      const uint32_t i = i0 + g + q;
+      const uint32_t r = ((i >= 2 ? i - 2 : 0) * cb) & 31;
+      U v;
+      if (W == 8) {
+        uint64_t top = (((uint64_t)ch[q][0] << 32) | ch[q][1]) << r;
+        top |= r ? (uint64_t)ch[q][NC - 1] >> (32 - r) : 0ull;
+        const uint64_t code = top >> (63 - b);
+        const uint64_t mag = code & ((1ull << b) - 1);
+        v = (U)(((code >> b) & 1) ? 0 - mag : mag);
+      } else {
+        const uint32_t top = r ? __builtin_amdgcn_alignbit(ch[q][0], ch[q][1], 32 - r) : ch[q][0];
+        const uint32_t code = top >> (31 - b);
+        const uint32_t mag = code & ((1u << b) - 1);
+        v = (U)(((code >> b) & 1) ? 0u - mag : mag);
+      }
+      e[g + q] = (i >= 2 && i < num) ? v : (U)0;
+    }
+  }
+  // per-thread aggregates, workgroup tuple scan
   U E = 0, Xs = 0;
-  if (i0 < num) {
-    DDReader rd;
-    rd.init(X, bs, s0);
-#pragma unroll 8
-    for (int k = 0; k < EP; k++) {
-      const uint64_t i = i0 + k;
-      U e = 0;
-      if (i >= 2 && i < num) e = (U)rd.template next<(W <= 4)>(b);
-      E += e;
-      Xs += E;
-      __builtin_amdgcn_sched_barrier(0);
-    }
+#pragma unroll
+  for (int k = 0; k < EP; k++) {
+    E += e[k];
+    Xs += E;
   }
-  uint64_t E64 = E, X64 = Xs;
-  block_ddscan_n(E64, X64, EP, L.red);
-  // pass 2: recompute codes, emit x into the slice registers
-  uint32_t r[SPD];
+  block_ddscan_u<U>(E, Xs, EP, (U*)L.red);
+  mark(7);  // diagnostics: code reads + scan
+  U d = dinit + E;
+  U x = xinit + (U)i0 * dinit + Xs;
 #pragma unroll
-  for (int k = 0; k < SPD; k++) r[k] = 0;
-  U d = dinit + (U)E64;
-  U x = xinit + (U)i0 * dinit + (U)X64;
-  if (i0 < num) {
-    DDReader rd;
-    rd.init(X, bs, s0);
+  for (int k = 0; k < EP; k++) {  // x in place of the codes (register pressure)
+    d += e[k];
+    x += d;
+    e[k] = x;
+  }
+  __syncthreads();  // every code read before the values overwrite them
+  {
+    const uint32_t s0 = tid_() * SP, n = num * W;
 #pragma unroll
-    for (int k = 0; k < EP; k++) {
-      const uint64_t i = i0 + k;
-      U e = 0;
-      if (i >= 2 && i < num) e = (U)rd.template next<(W <= 4)>(b);
-      d += e;
-      x += d;
-      rset<W>(r, k, (uint64_t)x);
-      __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < SP / 16; q++) {
+      const uint32_t o = s0 + 16 * q;
+      uint4 v;
+      if (W == 8) {
+        const uint64_t a = (uint64_t)e[2 * q], c = (uint64_t)e[2 * q + 1];
+        v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+      } else {
+        v = make_uint4((uint32_t)e[4 * q], (uint32_t)e[4 * q + 1], (uint32_t)e[4 * q + 2],
+                       (uint32_t)e[4 * q + 3]);
+      }
+      if (o < n) *(uint4*)(L.X + o) = v;
     }
   }
   __syncthreads();
-  slice_store(L, r, (uint32_t)(num * W));
+}
+
+// DoubleDelta data part for 32-bit values (codes <= 31 bits), in place.
+//  1. The bitstream's u64 words are rewritten into Y = X[16, 16 + 8*nw) in
+//     REVERSED word order (Y word j = stream word nw-1-j; one aligned 16-B
+//     unit per lane, gathered to registers, barrier, written back).
+//     MSB-first 32-bit chunk c of the stream then sits at Y dword K - c
+//     (K = 2*nw - 1), so chunks c and c+1 are the dword pair at K - c - 1
+//     whose little-endian 64-bit value is chunk_c:chunk_c+1 -- one
+//     ds_read2_b32 and one 64-bit shift extract any code.  (The last
+//     chunk's pair starts at Y dword -1: X[12, 16), hence the 16-B offset.)
+//  2. Each thread decodes its 32 consecutive codes into registers, the
+//     (E, X) tuple is scanned over the workgroup, x is emitted from the
+//     registers and stored back over X after a barrier.
+template <class M>
+__device__ __forceinline__ void dd_decode_part32(FastLds& L, uint32_t src, uint32_t b, uint32_t num,
+                                                 M&& mark) {
+  typedef uint32_t U;
+  constexpr int EP = SP / 4;  // 32 values per thread
+  constexpr int NU = (XCAP + 16 * FNT - 1) / (16 * FNT);
+  const uint8_t* X = L.X;
+  const U x0 = lds32(X, src + 9), x1 = lds32(X, src + 13);
+  const uint32_t bs = src + 17;
+  const uint32_t cb = b + 1;
+  const uint32_t nw = (uint32_t)(((uint64_t)(num - 2) * cb + 63) >> 6);  // words holding codes
+  const uint32_t t = tid_();
+  {
+    // 1. reversed-word copy of the stream to X[0, 8 nw)
+    const uint32_t nu = (nw + 1) >> 1;
+    uint32_t r[NU][4];
+#pragma unroll
+    for (int k = 0; k < NU; k++) {
+      const uint32_t u = t + k * FNT;
+      // Y words 2u, 2u+1 = stream words nw-1-2u, nw-2-2u: the 16 stream
+      // bytes starting at word nw-2-2u (clamped at the stream start; a
+      // missing word is never read by a code)
+      const int32_t w = (int32_t)nw - 2 - 2 * (int32_t)u;
+      const uint32_t o = bs + 8 * (uint32_t)(w < 0 ? 0 : w);
+      const uint32_t a = o & ~3u, sh = o & 3u;
+      uint32_t d[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) d[q] = *(const uint32_t*)(X + (a + 4 * q < XCAP ? a + 4 * q : 0));
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) v[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
+      // (word nw-2-2u, word nw-1-2u) -> (Y word 2u, Y word 2u+1) swapped
+      r[k][0] = v[2]; r[k][1] = v[3]; r[k][2] = v[0]; r[k][3] = v[1];
+      if (w < 0) { r[k][0] = v[0]; r[k][1] = v[1]; }  // odd nw: Y word 2u = stream word 0
+      (void)nu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NU; k++) {
+      const uint32_t u = t + k * FNT;
+      if (u < nu) *(uint4*)(L.X + 16 + 16 * u) = make_uint4(r[k][0], r[k][1], r[k][2], r[k][3]);
+    }
+    __syncthreads();
+  }
+  // 2. codes -> registers
+  const int32_t K1 = 2 * (int32_t)nw - 2;  // Y dword of chunk c+1 is K1 - c ... pair base
+  const uint32_t i0 = t * EP;
+  const uint32_t mb = b ? (1u << b) - 1 : 0u;
+  const uint32_t tsh = 64 - cb;
+  U e[EP];
+#pragma unroll
+  for (int g = 0; g < EP; g += 8) {
+    uint64_t V[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t i = i0 + g + q;
+      const uint32_t sb = (i >= 2 ? i - 2 : 0) * cb;
+      int32_t di = K1 - (int32_t)(sb >> 5);
+      di = di < -4 ? -4 : di;  // absent codes (i >= num) stay inside X
+      // two dwords, 4-B aligned only (ds_read2_b32, never an unaligned b64)
+      const uint32_t* Y32 = (const uint32_t*)(X + 16);
+      V[q] = ((uint64_t)Y32[di + 1] << 32) | Y32[di];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t i = i0 + g + q;
+      const uint32_t sb = (i >= 2 ? i - 2 : 0) * cb;
+      // V = chunk_c:chunk_c+1, the code at bit r = sb & 31 of chunk c
+      const uint32_t code = (uint32_t)(V[q] >> (tsh - (sb & 31)));
+      const uint32_t mag = code & mb;
+      const uint32_t neg = (uint32_t)__builtin_amdgcn_sbfe((int32_t)code, b, 1);  // 0 or ~0
+      const U v = (mag ^ neg) - neg;
+      e[g + q] = (i >= 2 && i < num) ? v : 0u;
+    }
+  }
+  U E = 0, Xs = 0;
+#pragma unroll
+  for (int k = 0; k < EP; k++) {
+    E += e[k];
+    Xs += E;
+  }
+  block_ddscan_u<U>(E, Xs, EP, (U*)L.red);
+  mark(7);  // diagnostics: realign + code reads + scan
+  const U dinit = x1 - x0, xinit = x0 - dinit;
+  U d = dinit + E;
+  U x = xinit + (U)i0 * dinit + Xs;
+#pragma unroll
+  for (int k = 0; k < EP; k++) {
+    d += e[k];
+    x += d;
+    e[k] = x;
+  }
+  __syncthreads();  // every code read before the values overwrite the stream
+  {
+    const uint32_t s0 = t * SP, n = num * 4;
+#pragma unroll
+    for (int q = 0; q < SP / 16; q++) {
+      const uint32_t o = s0 + 16 * q;
+      if (o < n) *(uint4*)(L.X + o) = make_uint4(e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]);
+    }
+  }
   __syncthreads();
+}
+
+template <int W, class M>
+__device__ __forceinline__ void dd_decode_part(FastLds& L, uint32_t src, uint32_t b, uint64_t num,
+                                               M&& mark) {
+  if (W == 4) dd_decode_part32(L, src, b, (uint32_t)num, mark);
+  else if (((src + 9 + 2 * W) & 3) == 0) dd_decode_part_t<W, true>(L, src, b, (uint32_t)num, mark);
+  else dd_decode_part_t<W, false>(L, src, b, (uint32_t)num, mark);
 }
 
 // ---------------------------------------------------------------------------
 // compression filter (DD / RLE) -- compression_filter.cc:303-347,413-486
 // ---------------------------------------------------------------------------
-template <int W>
-__device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
-                     uint8_t* gout, uint32_t cap);
 
 // Reads the compression md header (compression_filter.cc:323-347) into
 // L.pairs; returns false unless it is one data part plus <= 15 md parts that
@@ -1076,9 +1246,9 @@ __device__ bool comp_header(FastLds& L, View cur, uint32_t mo, uint32_t mn, uint
   return p <= cur.n && md_total <= MDCAP;
 }
 
-template <int W>
+template <int W, class M>
 __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
-                     uint8_t* gout, uint32_t cap) {
+                     uint8_t* gout, uint32_t cap, M&& mark) {
   // compression md header (compression_filter.cc:323-347) from a wave
   // snapshot of MD; part table: (un, cn) pairs, md parts first
   if (mn < 8) return false;
@@ -1105,7 +1275,12 @@ __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32
   if (raw) {
     if (c - 9 != u) return false;
   } else {
-    if (num < 3 || num * W != u || u > (uint32_t)(FNT * SP) || dd_check(c, u, W, b, num)) return false;
+    // b >= 1 and every word holding a code present: the reference's reads
+    // and writes all succeed (a sign bit ending a word forces the next word's
+    // read, which b >= 1 needs anyway; dd_compressor.cc:356-404)
+    if (num < 3 || num * W != u || u > (uint32_t)(FNT * SP) || b == 0) return false;
+    const uint64_t words = ((num - 2) * (uint64_t)(b + 1) + 63) >> 6;
+    if (9 + 2 * W + 8 * words > c) return false;
   }
   // metadata parts, serially, into MD[0, mdt).  When that range lies below
   // the compression header and the parts are in the snapshot (the usual
@@ -1113,13 +1288,25 @@ __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32
   // them (identical bytes from every wave; no barrier).  Otherwise thread 0
   // decodes from LDS between two barriers.
   if (mo >= mdt && in_snap) {
-    const bool l0 = (tid_() & 63) == 0;
+    const uint32_t lane = tid_() & 63;
+    const bool l0 = lane == 0;
     bool ok = true;
     uint32_t o = 0, ip = 0;
     for (uint32_t i = 0; i < nmd && ok; i++) {
       const uint32_t un = snap32(sm, 8 + 8 * i), cn = snap32(sm, 12 + 8 * i);
-      ok = dd_serial_g([&](uint32_t q) -> uint32_t { return snap8(sx, ip + q); }, cn,
-                       [&](uint32_t q, uint8_t v) { if (l0) L.MD[o + q] = v; }, un, W);
+      const uint32_t pb = cn >= 9 ? snap8(sx, ip) : 0u;
+      const uint64_t pn = cn >= 9 ? snapn(sx, ip + 1, 8) : 0ull;
+      // a raw part or one of <= 2 values is its bytes after the 9-byte
+      // header (dd_compressor.cc:327-347): lane-parallel copy
+      const bool plain = cn >= 9 && un <= 64 &&
+                         ((pb >= 8u * W - 1 && cn - 9 == un) ||
+                          (pn >= 1 && pn <= 2 && pn * W == un && cn >= 9 + un));
+      if (plain) {
+        if (lane < un) L.MD[o + lane] = L.X[cur.base + ip + 9 + lane];
+      } else {
+        ok = dd_serial_g([&](uint32_t q) -> uint32_t { return snap8(sx, ip + q); }, cn,
+                         [&](uint32_t q, uint8_t v) { if (l0) L.MD[o + q] = v; }, un, W);
+      }
       o += un;
       ip += cn;
     }
@@ -1148,7 +1335,8 @@ __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32
     if (final) final_copy(L, cur, gout);
     return true;
   }
-  dd_decode_part<W>(L, cur.base + src, b, num);
+  mark(4);  // diagnostics: DD header + metadata parts
+  dd_decode_part<W>(L, cur.base + src, b, num, mark);
   cur.base = 0;
   cur.n = u;
   if (final) final_copy(L, cur, gout);
@@ -1228,10 +1416,10 @@ __device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint3
 // inference see one small straight-line program.
 #define SC(kind, w, sg) ((kind) | ((w) << 4) | ((sg) << 8))
 
-template <int CODE, int POS>
+template <int CODE, int POS, class M>
 __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn,
                                           bool final, uint8_t* gout, uint32_t cap,
-                                          const tdbg_stage& s) {
+                                          const tdbg_stage& s, M&& mark) {
   constexpr int K = CODE & 15, W = (CODE >> 4) & 15, SG = (CODE >> 8) & 1;
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (K == TDBG_K_PASS) {
@@ -1249,7 +1437,7 @@ __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, u
   } else if constexpr (K == TDBG_K_PD) {
     return f_pd<W>(L, cur, mo, mn, final, gout, cap, s.dts);
   } else if constexpr (K == TDBG_K_DD) {
-    return f_dd<W>(L, cur, mo, mn, final, gout, cap);
+    return f_dd<W>(L, cur, mo, mn, final, gout, cap, mark);
   } else if constexpr (K == TDBG_K_RLE) {
     return f_rle(L, cur, mo, mn, final, gout, cap, (uint32_t)s.cs);
   } else {
@@ -1294,25 +1482,25 @@ __device__ __forceinline__ bool f_resident(const tdbg_plan& P, View cur, uint32_
   // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
   if constexpr (S3 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
-    if (!run_stage<S3, 3>(L, cur, mo, mn, false, gout, orig, P.s[3])) return false;
+    if (!run_stage<S3, 3>(L, cur, mo, mn, false, gout, orig, P.s[3], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(2);
   }
   if constexpr (S2 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S2, 2>(L, cur, mo, mn, false, gout, orig, P.s[2])) return false;
+    if (!run_stage<S2, 2>(L, cur, mo, mn, false, gout, orig, P.s[2], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 3 : 2);
   }
   if constexpr (S1 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S1, 1>(L, cur, mo, mn, false, gout, orig, P.s[1])) return false;
+    if (!run_stage<S1, 1>(L, cur, mo, mn, false, gout, orig, P.s[1], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 4 : S2 != 0 ? 3 : 2);
   }
   if (dbg_stop > 1) return true;
   hook();
-  const bool ok = run_stage<S0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0]);
+  const bool ok = run_stage<S0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0], mark);
   mark(5);
   return ok;
 }

@@ -10,7 +10,7 @@ import bench
 import workloads as W
 from tiledb_amd import engine
 
-NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c", "final", "tail", "-"]
+NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c|dd-hdr", "final", "tail", "dd-codes+scan"]
 _ser, _dt, _cs, _, _ = W.config("c5")
 dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)
