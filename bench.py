@@ -308,7 +308,8 @@ def main():
     if len(variants) > 1:
         line["config"]["variants"] = {
             v: {"GiBps": round(gibps(res[v]), 2), "roofline_frac": round(frac(res[v]), 4),
-                "kernel_ms": round(res[v]["kern_ms"], 4), "fallback_tiles_timed": res[v]["fallback"]}
+                "kernel_ms": round(res[v]["kern_ms"], 4), "fallback_tiles_timed": res[v]["fallback"],
+                "algorithmic_bytes_per_launch": int(res[v]["b_alg"])}
             for v in variants}
         line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v]) for v in variants), 2)
     if args.e2e:

@@ -1,0 +1,84 @@
+"""Summary of tools/profile_all.sh: per (config, variant) the fused kernel's
+rocprofv3 kernel-trace average over the timed launches, per-launch HBM
+traffic from the --pmc passes (KiB -> bytes; FETCH_SIZE doubled for gfx950
+16-B/lane streaming reads, MI355X_MICROARCH.md "HBM"), the algorithmic bytes
+and roofline fraction from the bench line of the same workload."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+PEAK = 8000.0
+
+
+def pmc(d, counter):
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "unfilter_fused_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                k = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
+    return list(per.values())
+
+
+def trace(d):
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        rows += [r for r in csv.DictReader(open(f)) if "unfilter_fused_kernel" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+
+
+def stats(d):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
+
+
+def main(out):
+    res = {}
+    for log in sorted(glob.glob(os.path.join(out, "bench_*.log"))):
+        cfg = os.path.basename(log)[6:-4]
+        lines = [l for l in open(log) if l.startswith("{")]
+        if not lines:
+            continue
+        line = json.loads(lines[-1])
+        variants = line["config"].get("variants") or {line["config"]["variant"]: {}}
+        for v in variants:
+            key = f"{cfg}_{v}"
+            e = {"bench_GiBps": variants[v].get("GiBps", line["value"]) if variants[v] else line["value"]}
+            d = trace(os.path.join(out, f"trace_{cfg}_{v}"))
+            if len(d) >= 24:
+                timed = d[-20:]  # sync pass + warmup first, then the 20 timed launches
+                e["rocprof_fused_kernel_avg_us"] = round(statistics.mean(timed), 2)
+            f = pmc(os.path.join(out, f"pmc_{cfg}_{v}_FETCH_SIZE"), "FETCH_SIZE")
+            w = pmc(os.path.join(out, f"pmc_{cfg}_{v}_WRITE_SIZE"), "WRITE_SIZE")
+            if f and w:
+                fk, wk = statistics.median(f), statistics.median(w)
+                e.update({"fetch_size_kib_median": fk, "write_size_kib_median": wk,
+                          "hbm_read_bytes_per_launch": int(2 * fk * 1024),
+                          "hbm_write_bytes_per_launch": int(wk * 1024),
+                          "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024),
+                          "correction": "read = 2 x FETCH_SIZE (gfx950 16B/lane streaming read), KiB -> bytes"})
+            res[key] = e
+        for v in variants:
+            h = f"{cfg}_{v}"
+            b_alg = (variants[v] or {}).get("algorithmic_bytes_per_launch") or \
+                line["roofline"]["algorithmic_bytes_per_launch"]
+            res[h]["algorithmic_bytes_per_launch"] = b_alg
+            if "rocprof_fused_kernel_avg_us" in res[h]:
+                ach = b_alg / (res[h]["rocprof_fused_kernel_avg_us"] * 1e-6) / 1e9
+                res[h]["rocprof_achieved_GBps"] = round(ach, 1)
+                res[h]["rocprof_roofline_frac"] = round(ach / PEAK, 4)
+            if "hbm_bytes_per_launch" in res[h]:
+                res[h]["traffic_over_algorithmic"] = round(res[h]["hbm_bytes_per_launch"] / b_alg, 4)
+        res[f"{cfg}_{line['config']['variant']}"]["bench_line"] = line
+    json.dump(res, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
