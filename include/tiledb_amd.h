@@ -233,6 +233,36 @@ int tdbg_unfilter_tiles_cpu(const tdbg_pipeline* p, uint64_t ntiles,
                             const uint64_t* out_size, uint32_t flags,
                             int32_t* host_status, uint32_t nthreads);
 
+/* ---- forward (filter) direction: the write path ---------------------------
+ * Replaces WriterBase::filter_tile -> FilterPipeline::run_forward
+ * (writer_base.cc:870-915, filter_pipeline.cc:382-426; chunks
+ * filter_pipeline.cc:208-369, WriterTile::compute_chunk_size tile.cc:87-100)
+ * for fixed-size tiles: each unfiltered tile d_in[i] (d_in_size[i] bytes) is
+ * chunked (max_chunk = 0: 64 KiB, constants.cc:730), run through every
+ * filter's run_forward and written in the on-disk layout
+ * [u64 nchunks]([u32 orig][u32 filtered][u32 md][md][data])* to d_out[i]
+ * (capacity d_out_cap[i], tdbg_filtered_bound() always suffices); its length
+ * goes to d_out_len[i].  Device arrays, like tdbg_unfilter_tiles_async.
+ * Statuses: TDBG_E_PD_DECREASING, TDBG_E_DD_OVERFLOW, TDBG_E_RLE_FORMAT,
+ * TDBG_E_DD_TYPE / TDBG_E_DELTA_TYPE, TDBG_E_OUT_FULL (capacity), TDBG_E_ARG
+ * (a BWR / PD window smaller than one value: a division by zero in the
+ * reference).  The BWR offset of a window whose range overflows T is
+ * uninitialized in the reference (bit_width_reduction_filter.cc:421-430)
+ * and written as 0 here. */
+uint64_t tdbg_filtered_bound(const tdbg_pipeline* p, uint64_t tile_size, uint32_t max_chunk);
+int tdbg_filter_tiles_async(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t ntiles,
+                            const uint8_t* const* d_in, const uint64_t* d_in_size,
+                            uint8_t* const* d_out, const uint64_t* d_out_cap,
+                            uint64_t* d_out_len, uint32_t max_chunk, int32_t* d_status,
+                            tdbg_stream stream);
+/* Same, synchronous; statuses to host_status (may be NULL); returns the first
+ * failing tile's status. */
+int tdbg_filter_tiles_sync(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t ntiles,
+                           const uint8_t* const* d_in, const uint64_t* d_in_size,
+                           uint8_t* const* d_out, const uint64_t* d_out_cap,
+                           uint64_t* d_out_len, uint32_t max_chunk, int32_t* host_status,
+                           tdbg_stream stream);
+
 /* Stats mirrored from the reference (filter_pipeline.cc:490-491,
  * reader_base.cc:1074): cumulative since context creation.  tiles_unfiltered
  * counts tiles submitted; read_unfiltered_byte_num counts the unfiltered bytes

@@ -1,0 +1,128 @@
+"""GPU parity of the forward (filter) direction: tdbg_filter_tiles_* against
+the oracle's FilterPipeline::run_forward restatement (oracle_filter_tile) --
+bit-exact filtered tiles, identical statuses on inputs the reference rejects,
+and the round trip through the device unfilter.  The BWR offset of a window
+whose range overflows T (uninitialized in the reference,
+bit_width_reduction_filter.cc:421-430) is written as 0 by both sides, so
+those bytes compare exactly here but are parity-unpinned against the
+reference itself.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from tests.cases import config_cases, edge_cases, fused_spec_cases, random_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from tiledb_amd import engine
+    return engine
+
+
+@pytest.fixture(scope="module")
+def ctx(eng):
+    return eng.Context(0)
+
+
+def forward_parity(eng, ctx, O, case, roundtrip=True):
+    if case.offsets:
+        pytest.skip("var-size chunking (offsets) is not on the forward device path")
+    op = O.OraclePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    st, got = ctx.filter(dp, case.tiles, max_chunk=case.max_chunk)
+    for i, t in enumerate(case.tiles):
+        try:
+            ref = np.frombuffer(op.filter_tile(t, None, case.max_chunk), dtype=np.uint8)
+            rc = 0
+        except O.OracleError as e:
+            ref, rc = None, e.code
+        assert int(st[i]) == rc, f"{case.name} tile {i}: gpu status {st[i]} oracle {rc}"
+        if rc:
+            continue
+        if not np.array_equal(got[i], ref):
+            n = min(got[i].size, ref.size)
+            bad = np.nonzero(got[i][:n] != ref[:n])[0]
+            raise AssertionError(f"{case.name} tile {i}: sizes {got[i].size}/{ref.size}, "
+                                 f"{bad.size} bytes differ, first at {bad[:1]}")
+    if roundtrip:
+        ok = [i for i in range(len(case.tiles)) if st[i] == 0]
+        if ok:
+            osz = [case.tiles[i].size + (8 if case.offsets_tile else 0) for i in ok]
+            batch = eng.TileBatch.from_host([got[i] for i in ok], osz)
+            rst = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile)
+            assert not rst.any()
+            for k, i in enumerate(ok):
+                # lossy stages (float scale) do not restore the input: the
+                # round trip is checked against the oracle's unfilter instead
+                urc, want = op.unfilter_tile(got[i], osz[k], case.offsets_tile)
+                assert urc == 0
+                assert np.array_equal(batch.output(k)[: case.tiles[i].size], want[: case.tiles[i].size])
+    return st
+
+
+_CONFIG = config_cases(3)
+_EDGE = edge_cases()
+_SPECS = fused_spec_cases(2)
+
+
+@pytest.mark.parametrize("case", _CONFIG + _SPECS, ids=[c.name for c in _CONFIG + _SPECS])
+def test_forward_config_parity(eng, ctx, oracle_mod, case):
+    forward_parity(eng, ctx, oracle_mod, case)
+
+
+@pytest.mark.parametrize("case", _EDGE, ids=[c.name for c in _EDGE])
+def test_forward_edge_parity(eng, ctx, oracle_mod, case):
+    forward_parity(eng, ctx, oracle_mod, case)
+
+
+def test_forward_random_pipelines(eng, ctx, oracle_mod):
+    n = 0
+    for case in random_cases(120):
+        if case.offsets:
+            continue
+        forward_parity(eng, ctx, oracle_mod, case)
+        n += 1
+    assert n > 100
+
+
+def test_forward_rejections(eng, ctx, oracle_mod):
+    """Inputs the reference rejects on write: decreasing positive-delta data,
+    DoubleDelta int64 overflow, DoubleDelta on floats (statuses equal the oracle's)."""
+    from tests.cases import Case, P, DD, RLE, as_u8
+    from tiledb_amd.filter_pipeline import Datatype, PositiveDeltaFilter
+    cases = [
+        Case("pd_decreasing", P(PositiveDeltaFilter(64)), Datatype.UINT32, 4,
+             [as_u8(np.array([5, 4, 3] * 50, dtype=np.uint32))]),
+        Case("dd_overflow_i64", P(DD()), Datatype.INT64, 8,
+             [as_u8(np.array([-2**63, 2**63 - 1, 0, 5], dtype=np.int64))]),
+        Case("dd_float", P(DD()), Datatype.FLOAT32, 4, [as_u8(np.arange(100, dtype=np.float32))]),
+    ]
+    for c in cases:
+        st = forward_parity(eng, ctx, oracle_mod, c, roundtrip=False)
+        assert st[0] != 0, c.name
+    # a tile that is not a multiple of the cell is chunked at cell multiples
+    # (the 2-byte tail chunk holds no whole cell): accepted by both sides
+    c = Case("rle_ragged", P(RLE()), Datatype.UINT8, 4, [np.arange(10, dtype=np.uint8)])
+    assert forward_parity(eng, ctx, oracle_mod, c, roundtrip=False)[0] == 0
+
+
+def test_forward_full_size_c5(eng, ctx, oracle_mod):
+    """A BASELINE C5 shard's worth of tiles (2,000 x 64 KiB, active + ramp +
+    rand): forward on the device, every tile equal to the oracle's bytes and
+    the device round trip restores the values."""
+    import workloads as W
+    from tests.cases import c5_tiles, P, DD, Case
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
+    rng = np.random.default_rng(4)
+    uniq = (c5_tiles(8, "ramp") + c5_tiles(8, "rand") +
+            [W.c5_values("active", k, rng).view(np.uint8) for k in range(16)])
+    tiles = [uniq[i % len(uniq)] for i in range(2000)]
+    case = Case("c5_full", P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256)), Datatype.INT32, 4,
+                tiles)
+    forward_parity(eng, ctx, oracle_mod, case)

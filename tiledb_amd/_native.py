@@ -52,6 +52,11 @@ SIGNATURES = {
                                                      ctypes.c_uint64]),
     "tdbg_unfilter_tiles_cpu": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
                                                ctypes.c_uint32, c_i32p, ctypes.c_uint32]),
+    "tdbg_filtered_bound": (ctypes.c_uint64, [c_vp, ctypes.c_uint64, ctypes.c_uint32]),
+    "tdbg_filter_tiles_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               ctypes.c_uint32, c_vp, c_vp]),
+    "tdbg_filter_tiles_sync": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                              ctypes.c_uint32, c_i32p, c_vp]),
     "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
     "tdbg_context_path_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),

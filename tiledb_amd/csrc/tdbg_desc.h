@@ -92,6 +92,11 @@ struct KParams {
   // add per workgroup at exit.
   uint64_t* stats;
   uint64_t* prof;     // diagnostics: per-workgroup phase clocks (TDBG_PROF_PHASES), or null
+  // forward (filter) launches: per-tile filtered length out, Tile::cell_size
+  // and WriterTile's max chunk size (0 = 64 KiB) for compute_chunk_size
+  uint64_t* out_len;
+  uint64_t cell_size;
+  uint32_t max_chunk;
   tdbg_plan plan;
 };
 

@@ -27,6 +27,7 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
                                           hipStream_t stream);
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
+extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
 #define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
 #define TDBG_DECL_PART(k) \
   extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
@@ -125,6 +126,10 @@ struct tdbg_context {
   uint32_t slot_cap = 80 * 1024, md_cap = 16 * 1024, tab_cap = 32 * 1024;
   uint8_t* rscratch = nullptr;
   uint64_t rscratch_bytes = 0;
+  // forward (filter) scratch slots
+  uint8_t* fscratch = nullptr;
+  uint64_t fscratch_bytes = 0;
+  uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
   uint64_t* d_need = nullptr;
@@ -312,6 +317,9 @@ void build_plan(tdbg_pipeline* p) {
               t == TDBG_STRING_UTF32 || t == TDBG_STRING_UCS2 || t == TDBG_STRING_UCS4 ||
               t == TDBG_ANY)
             s.w = 1;  // DoubleDelta::decompress<uint8_t> (dd_compressor.cc:187-194)
+          // signedness of T (the forward pass's checked deltas, dd_compressor.cc:63-127)
+          s.sgn = (t == TDBG_INT8 || t == TDBG_CHAR || t == TDBG_INT16 || t == TDBG_INT32 ||
+                   t == TDBG_INT64 || is_dt_time(t)) ? 1 : 0;
         } else {
           s.kind = TDBG_K_UNSUPPORTED;
           p->supported = false;
@@ -500,6 +508,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_fbq) (void)hipFree(c->d_fbq);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->rscratch) (void)hipFree(c->rscratch);
+  if (c->fscratch) (void)hipFree(c->fscratch);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -714,6 +723,163 @@ static int read_stats(const tdbg_context* c, uint64_t (&h)[TDBG_STAT_N]) {
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  return TDBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// forward (filter) direction: FilterPipeline::run_forward
+// ---------------------------------------------------------------------------
+static uint64_t fwd_chunk_bound(uint64_t tile_size, uint64_t cell, uint32_t max_chunk) {
+  const uint64_t mc = max_chunk ? max_chunk : 65536;
+  uint64_t c = std::min<uint64_t>(mc, tile_size);
+  c = c / (cell ? cell : 1) * (cell ? cell : 1);
+  return std::max<uint64_t>(c, cell ? cell : 1);
+}
+
+uint64_t tdbg_filtered_bound(const tdbg_pipeline* p, uint64_t tile_size, uint32_t max_chunk) {
+  if (!p) return 0;
+  const uint64_t chunk = fwd_chunk_bound(tile_size, p->cell_size, max_chunk);
+  const uint64_t nch = tile_size / chunk + 2;
+  // per chunk: header, per-filter metadata (windows of >= 1 element: at most
+  // 13 B per element), RLE growth (3x for 1-byte cells), DD/DELTA headers
+  const uint64_t nf = p->filters.size();
+  return 8 + nch * (12 + 64 + 64 * nf) + tile_size * 3 + (tile_size / 2 + 64) * 13 * std::min<uint64_t>(nf, 4) +
+         4096;
+}
+
+static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, const uint8_t* const* d_in,
+                         const uint64_t* d_in_size, uint8_t* const* d_out, const uint64_t* d_out_cap,
+                         uint64_t* d_out_len, uint32_t max_chunk, int32_t* d_status, uint64_t* d_need,
+                         const uint32_t* d_list, uint8_t* scratch, uint64_t slot_bytes, uint32_t slot_cap,
+                         uint32_t md_cap, uint32_t tab_cap, uint32_t grid, hipStream_t s) {
+  tdbg::KParams kp{};
+  kp.in = d_in;
+  kp.in_size = d_in_size;
+  kp.out = d_out;
+  kp.out_size = d_out_cap;
+  kp.out_len = d_out_len;
+  kp.status = d_status;
+  kp.need = d_need;
+  kp.tile_list = d_list;
+  kp.ntiles = n;
+  kp.plan = p->plan;
+  kp.cell_size = p->cell_size;
+  kp.max_chunk = max_chunk;
+  kp.scratch = scratch;
+  kp.slot_bytes = slot_bytes;
+  kp.slot_cap = slot_cap;
+  kp.md_cap = md_cap;
+  kp.tab_cap = tab_cap;
+  hipError_t e = tdbg_launch_filter(&kp, grid, s);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("filter launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+// forward scratch: per workgroup 2 data buffers (3 x chunk: RLE growth),
+// 2 metadata buffers, a window / run table
+static void fwd_caps(uint64_t chunk, uint32_t* slot, uint32_t* md, uint32_t* tab) {
+  *slot = (uint32_t)(((3 * chunk + 4096) + 255) & ~255ull);
+  *md = (uint32_t)(((chunk + 4096) + 255) & ~255ull);
+  *tab = (uint32_t)(((8 * chunk + 256) + 255) & ~255ull);
+}
+
+int tdbg_filter_tiles_async(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                            const uint8_t* const* d_in, const uint64_t* d_in_size, uint8_t* const* d_out,
+                            const uint64_t* d_out_cap, uint64_t* d_out_len, uint32_t max_chunk,
+                            int32_t* d_status, tdbg_stream stream) {
+  if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (ntiles == 0) return TDBG_OK;
+  if (!d_in || !d_in_size || !d_out || !d_out_cap || !d_out_len)
+    return fail(TDBG_E_ARG, "null tile arrays");
+  if (ntiles > 0xffffffffull) return fail(TDBG_E_ARG, "too many tiles in one call");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  rc = ensure_status(c, ntiles);
+  if (rc) return rc;
+  const uint64_t chunk = fwd_chunk_bound(max_chunk ? max_chunk : 65536, p->cell_size, max_chunk);
+  uint32_t sc, mc, tc;
+  fwd_caps(chunk, &sc, &mc, &tc);
+  const uint64_t sb = 2ull * sc + 2ull * mc + tc;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 2);
+  if (sb * grid > c->fscratch_bytes) {
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    if (c->fscratch) HIP_OK(hipFree(c->fscratch));
+    c->fscratch = nullptr;
+    c->fscratch_bytes = 0;
+    HIP_OK(hipMalloc(&c->fscratch, sb * grid));
+    c->fscratch_bytes = sb * grid;
+  }
+  rc = filter_launch(c, p, ntiles, d_in, d_in_size, d_out, d_out_cap, d_out_len, max_chunk,
+                     d_status ? d_status : c->d_status, c->d_need, nullptr, c->fscratch, sb, sc, mc, tc, grid,
+                     (hipStream_t)stream);
+  return rc;
+}
+
+int tdbg_filter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                           const uint8_t* const* d_in, const uint64_t* d_in_size, uint8_t* const* d_out,
+                           const uint64_t* d_out_cap, uint64_t* d_out_len, uint32_t max_chunk,
+                           int32_t* host_status, tdbg_stream stream) {
+  if (ntiles == 0) return TDBG_OK;
+  int rc = tdbg_filter_tiles_async(c, p, ntiles, d_in, d_in_size, d_out, d_out_cap, d_out_len, max_chunk,
+                                   c ? c->d_status : nullptr, stream);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int32_t> st(ntiles);
+  std::vector<uint64_t> need(ntiles);
+  HIP_OK(hipMemcpyAsync(st.data(), c->d_status, ntiles * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(need.data(), c->d_need, ntiles * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  // TDBG_E_SCRATCH: a stage outgrew the default slots (tiny BWR/PD windows,
+  // RLE of 1-byte cells ...); redo those tiles with retry-only slots
+  for (int pass = 0; pass < 2 * TDBG_MAX_FILTERS + 2; pass++) {
+    std::vector<uint32_t> list;
+    uint64_t maxneed = 0;
+    for (uint64_t i = 0; i < ntiles; i++)
+      if (st[i] == TDBG_E_SCRATCH) { list.push_back((uint32_t)i); maxneed = std::max(maxneed, need[i]); }
+    if (list.empty()) break;
+    const uint64_t grow = ((maxneed + maxneed / 2 + 4096) + 255) & ~255ull;
+    if (grow > 0xffffffffull / 4) return fail(TDBG_E_SCRATCH, "chunk stage larger than 1 GiB");
+    const uint64_t chunk = fwd_chunk_bound(max_chunk ? max_chunk : 65536, p->cell_size, max_chunk);
+    uint32_t sc, mc, tc;
+    fwd_caps(chunk, &sc, &mc, &tc);
+    sc = (uint32_t)std::max<uint64_t>(sc, grow);
+    mc = (uint32_t)std::max<uint64_t>(mc, grow);
+    tc = (uint32_t)std::max<uint64_t>(tc, grow);
+    c->fwd_retry_caps[0] = std::max(c->fwd_retry_caps[0], sc);
+    const uint64_t sb = 2ull * sc + 2ull * mc + tc;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(list.size(), (256ull << 20) / sb));
+    if (list.size() > c->list_cap) {
+      if (c->d_list) HIP_OK(hipFree(c->d_list));
+      c->d_list = nullptr;
+      c->list_cap = 0;
+      HIP_OK(hipMalloc(&c->d_list, list.size() * 4));
+      c->list_cap = list.size();
+    }
+    HIP_OK(hipMemcpyAsync(c->d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
+    if (sb * grid > c->rscratch_bytes) {
+      HIP_OK(hipStreamSynchronize(s));
+      if (c->rscratch) HIP_OK(hipFree(c->rscratch));
+      c->rscratch = nullptr;
+      c->rscratch_bytes = 0;
+      HIP_OK(hipMalloc(&c->rscratch, sb * grid));
+      c->rscratch_bytes = sb * grid;
+    }
+    rc = filter_launch(c, p, list.size(), d_in, d_in_size, d_out, d_out_cap, d_out_len, max_chunk, c->d_status,
+                       c->d_need, c->d_list, c->rscratch, sb, sc, mc, tc, grid, s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(st.data(), c->d_status, ntiles * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(need.data(), c->d_need, ntiles * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  if (host_status) memcpy(host_status, st.data(), ntiles * 4);
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (st[i]) {
+      char msg[160];
+      snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
+      return fail(st[i], msg);
+    }
   return TDBG_OK;
 }
 

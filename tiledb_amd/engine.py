@@ -195,6 +195,41 @@ class Context:
             TILE_OFFSETS if offsets_tiles else 0, batch.d_status.data_ptr(),
             self._stream(stream)), "tdbg_unfilter_tiles_async")
 
+    def filter(self, dp: DevicePipeline, tiles: Sequence, max_chunk: int = 0, stream=None):
+        """Forward direction (FilterPipeline::run_forward): unfiltered tiles ->
+        on-disk filtered tiles.  Returns (statuses, [filtered bytes as np.uint8])."""
+        import torch
+        bufs = [np.ascontiguousarray(t).view(np.uint8).reshape(-1) for t in tiles]
+        n = len(bufs)
+        sizes = np.array([b.size for b in bufs], dtype=np.uint64)
+        offs = pack_offsets(sizes, 1)
+        packed = np.zeros(int(offs[-1] + sizes[-1]) + 1 if n else 1, dtype=np.uint8)
+        for b, o in zip(bufs, offs):
+            packed[int(o):int(o) + b.size] = b
+        dev = torch.device("cuda", self.device)
+        d_in = torch.from_numpy(packed).to(dev)
+        caps = np.array([lib.tdbg_filtered_bound(dp.h, int(sz), max_chunk) for sz in sizes], dtype=np.uint64)
+        ooff = pack_offsets(caps, 16)
+        d_out = torch.zeros(int(ooff[-1] + caps[-1]) + 16 if n else 16, dtype=torch.uint8, device=dev)
+        meta = np.empty((5, max(n, 1)), dtype=np.uint64)
+        meta[0, :n] = offs + np.uint64(d_in.data_ptr())
+        meta[1, :n] = sizes
+        meta[2, :n] = ooff + np.uint64(d_out.data_ptr())
+        meta[3, :n] = caps
+        meta[4, :n] = 0
+        d_meta = torch.from_numpy(meta.view(np.int64)).to(dev)
+        base, k = d_meta.data_ptr(), max(n, 1) * 8
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        rc = lib.tdbg_filter_tiles_sync(self.h, dp.h, n, base, base + k, base + 2 * k, base + 3 * k, base + 4 * k,
+                                        max_chunk, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                        self._stream(stream))
+        if rc and not st[:n].any():
+            _check(rc, "tdbg_filter_tiles_sync")
+        lens = d_meta[4].cpu().numpy().view(np.uint64)[:n]
+        out = d_out.cpu().numpy()
+        res = [out[int(o):int(o) + int(l)].copy() for o, l in zip(ooff, lens)]
+        return st[:n], res
+
     def path_stats(self):
         """(fused, fallback, general) tile counts, cumulative (synchronizes the device)."""
         f, b, g = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
