@@ -124,6 +124,55 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0)
 
 
+def time_forward(engine, ctx, dp, vals, idx, pool, steps: int, warmup: int, dist):
+    """Forward direction (tdbg_filter_tiles_async) over the same tiles'
+    unfiltered values, device-resident: wall time of `steps` launches (barrier
+    + synchronize on both sides, max over ranks) and the mean launch time from
+    HIP events on the launch stream.  After the timed region every tile's
+    statuses are OK and its filtered bytes equal the workload encoder's."""
+    import torch
+    fb = ctx.filter_batch(dp, [vals[i] for i in idx])
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, warmup)):
+        ctx.filter_async(dp, fb, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    fb.d_status.fill_(-1)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        ctx.filter_async(dp, fb, stream=stream.cuda_stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st = fb.d_status[: fb.ntiles].cpu().numpy()
+    if st.any():
+        raise SystemExit(f"forward: device status nonzero: {np.unique(st)}")
+    lens = fb.lengths()
+    want = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
+    if not np.array_equal(lens, want):
+        raise SystemExit("forward: filtered sizes differ from the encoder's")
+    step = 1024
+    for a in range(0, fb.ntiles, step):
+        b = min(fb.ntiles, a + step)
+        lo, hi = int(fb.out_off[a]), int(fb.out_off[b - 1] + lens[b - 1])
+        host = fb.d_out[lo:hi].cpu().numpy()
+        for k in range(a, b):
+            o = int(fb.out_off[k]) - lo
+            if host[o:o + int(lens[k])].tobytes() != bytes(pool[idx[k]]):
+                raise SystemExit(f"forward: tile {k} differs from the encoder's filtered bytes")
+    if dist is not None:
+        elapsed = max_over_ranks(dist, elapsed, "cuda")
+    b_alg = float(fb.in_size.sum() + lens.sum())
+    return elapsed, kern_ms, b_alg, float(fb.in_size.sum())
+
+
 def max_over_ranks(dist, x: float, device: str) -> float:
     """The job's time is its slowest rank's (all_reduce MAX; tests run it on gloo)."""
     import torch
@@ -203,6 +252,9 @@ def main():
                     help="also time host-resident end-to-end (default on; every rank, "
                          "total over ranks / max-over-ranks time)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    ap.add_argument("--forward", action="store_true", default=True,
+                    help="also time the forward (filter) direction on the headline variant (default on)")
+    ap.add_argument("--no-forward", dest="forward", action="store_false")
     ap.add_argument("--e2e-batch-mb", type=int, default=64,
                     help="host E2E staging batch (MiB per side; 2 batches in flight)")
     args = ap.parse_args()
@@ -248,6 +300,8 @@ def main():
         res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
                         out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback,
                         packed=packed, offs=offs, sizes=sizes)
+        if args.forward and vi == 0 and not ablation:
+            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, args.steps, args.warmup, dist)
         if args.e2e:
             res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args,
                                   dist, world)
@@ -312,6 +366,18 @@ def main():
                 "algorithmic_bytes_per_launch": int(res[v]["b_alg"])}
             for v in variants}
         line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v]) for v in variants), 2)
+    if "fwd" in r:
+        el, fk, fb_alg, fin = r["fwd"]
+        line["forward"] = {
+            "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
+            "value": round(fin * world / (el / args.steps) / 2**30, 2),
+            "unit": "GiB/s",
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "kernel": "filter_tiles_kernel",
+            "kernel_ms": round(fk, 4),
+            "algorithmic_bytes_per_launch": int(fb_alg),
+            "roofline_frac": round(fb_alg / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
     if args.e2e:
         line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -802,7 +802,7 @@ int tdbg_filter_tiles_async(tdbg_context* c, const tdbg_pipeline* p, uint64_t nt
   uint32_t sc, mc, tc;
   fwd_caps(chunk, &sc, &mc, &tc);
   const uint64_t sb = 2ull * sc + 2ull * mc + tc;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 2);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
   if (sb * grid > c->fscratch_bytes) {
     HIP_OK(hipStreamSynchronize((hipStream_t)stream));
     if (c->fscratch) HIP_OK(hipFree(c->fscratch));

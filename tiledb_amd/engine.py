@@ -152,6 +152,54 @@ class TileBatch:
         return self.d_out.cpu().numpy()
 
 
+class FilterBatch:
+    """Device-resident forward batch: unfiltered tiles packed back to back in
+    `d_in`, each filtered tile written at a 16-byte aligned slot of `d_out`
+    sized by tdbg_filtered_bound; `d_meta` rows are the C-ABI's pointer /
+    size / capacity / filtered-length arrays."""
+
+    def __init__(self, dp: DevicePipeline, tiles: Sequence, device: int, max_chunk: int = 0):
+        import torch
+        bufs = [np.ascontiguousarray(t).view(np.uint8).reshape(-1) for t in tiles]
+        n = len(bufs)
+        self.max_chunk = int(max_chunk)
+        self.in_size = np.array([b.size for b in bufs], dtype=np.uint64)
+        offs = pack_offsets(self.in_size, 1)
+        packed = np.zeros(int(offs[-1] + self.in_size[-1]) + 1 if n else 1, dtype=np.uint8)
+        for b, o in zip(bufs, offs):
+            packed[int(o):int(o) + b.size] = b
+        dev = torch.device("cuda", device)
+        self.d_in = torch.from_numpy(packed).to(dev)
+        self.cap = np.array([lib.tdbg_filtered_bound(dp.h, int(sz), self.max_chunk) for sz in self.in_size],
+                            dtype=np.uint64)
+        self.out_off = pack_offsets(self.cap, 16)
+        self.d_out = torch.zeros(int(self.out_off[-1] + self.cap[-1]) + 16 if n else 16, dtype=torch.uint8,
+                                 device=dev)
+        meta = np.zeros((5, max(n, 1)), dtype=np.uint64)
+        meta[0, :n] = offs + np.uint64(self.d_in.data_ptr())
+        meta[1, :n] = self.in_size
+        meta[2, :n] = self.out_off + np.uint64(self.d_out.data_ptr())
+        meta[3, :n] = self.cap
+        self.d_meta = torch.from_numpy(meta.view(np.int64)).to(dev)
+        self.d_status = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+
+    @property
+    def ntiles(self) -> int:
+        return int(self.in_size.size)
+
+    def ptrs(self):
+        base, k = self.d_meta.data_ptr(), max(self.ntiles, 1) * 8
+        return base, base + k, base + 2 * k, base + 3 * k, base + 4 * k
+
+    def lengths(self) -> np.ndarray:
+        return self.d_meta[4].cpu().numpy().view(np.uint64)[: self.ntiles].copy()
+
+    def outputs(self):
+        lens = self.lengths()
+        out = self.d_out.cpu().numpy()
+        return [out[int(o):int(o) + int(l)].copy() for o, l in zip(self.out_off, lens)]
+
+
 class Context:
     """tdbg_context: per-device scratch, status arrays, timing."""
 
@@ -195,40 +243,32 @@ class Context:
             TILE_OFFSETS if offsets_tiles else 0, batch.d_status.data_ptr(),
             self._stream(stream)), "tdbg_unfilter_tiles_async")
 
+    def filter_batch(self, dp: DevicePipeline, tiles: Sequence, max_chunk: int = 0) -> "FilterBatch":
+        """Device-resident forward batch: the unfiltered tiles packed back to
+        back on this context's device, outputs sized by tdbg_filtered_bound."""
+        return FilterBatch(dp, tiles, self.device, max_chunk)
+
+    def filter_async(self, dp: DevicePipeline, fb: "FilterBatch", stream=None) -> None:
+        """tdbg_filter_tiles_async over a FilterBatch (statuses and filtered
+        lengths stay on the device)."""
+        pin, psz, pout, pcap, plen = fb.ptrs()
+        _check(lib.tdbg_filter_tiles_async(self.h, dp.h, fb.ntiles, pin, psz, pout, pcap, plen,
+                                           fb.max_chunk, fb.d_status.data_ptr(), self._stream(stream)),
+               "tdbg_filter_tiles_async")
+
     def filter(self, dp: DevicePipeline, tiles: Sequence, max_chunk: int = 0, stream=None):
         """Forward direction (FilterPipeline::run_forward): unfiltered tiles ->
         on-disk filtered tiles.  Returns (statuses, [filtered bytes as np.uint8])."""
-        import torch
-        bufs = [np.ascontiguousarray(t).view(np.uint8).reshape(-1) for t in tiles]
-        n = len(bufs)
-        sizes = np.array([b.size for b in bufs], dtype=np.uint64)
-        offs = pack_offsets(sizes, 1)
-        packed = np.zeros(int(offs[-1] + sizes[-1]) + 1 if n else 1, dtype=np.uint8)
-        for b, o in zip(bufs, offs):
-            packed[int(o):int(o) + b.size] = b
-        dev = torch.device("cuda", self.device)
-        d_in = torch.from_numpy(packed).to(dev)
-        caps = np.array([lib.tdbg_filtered_bound(dp.h, int(sz), max_chunk) for sz in sizes], dtype=np.uint64)
-        ooff = pack_offsets(caps, 16)
-        d_out = torch.zeros(int(ooff[-1] + caps[-1]) + 16 if n else 16, dtype=torch.uint8, device=dev)
-        meta = np.empty((5, max(n, 1)), dtype=np.uint64)
-        meta[0, :n] = offs + np.uint64(d_in.data_ptr())
-        meta[1, :n] = sizes
-        meta[2, :n] = ooff + np.uint64(d_out.data_ptr())
-        meta[3, :n] = caps
-        meta[4, :n] = 0
-        d_meta = torch.from_numpy(meta.view(np.int64)).to(dev)
-        base, k = d_meta.data_ptr(), max(n, 1) * 8
+        fb = self.filter_batch(dp, tiles, max_chunk)
+        n = fb.ntiles
         st = np.zeros(max(n, 1), dtype=np.int32)
-        rc = lib.tdbg_filter_tiles_sync(self.h, dp.h, n, base, base + k, base + 2 * k, base + 3 * k, base + 4 * k,
-                                        max_chunk, st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+        pin, psz, pout, pcap, plen = fb.ptrs()
+        rc = lib.tdbg_filter_tiles_sync(self.h, dp.h, n, pin, psz, pout, pcap, plen, max_chunk,
+                                        st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                         self._stream(stream))
         if rc and not st[:n].any():
             _check(rc, "tdbg_filter_tiles_sync")
-        lens = d_meta[4].cpu().numpy().view(np.uint64)[:n]
-        out = d_out.cpu().numpy()
-        res = [out[int(o):int(o) + int(l)].copy() for o, l in zip(ooff, lens)]
-        return st[:n], res
+        return st[:n], fb.outputs()
 
     def path_stats(self):
         """(fused, fallback, general) tile counts, cumulative (synchronizes the device)."""
