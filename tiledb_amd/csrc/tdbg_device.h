@@ -60,13 +60,39 @@ __host__ __device__ __forceinline__ uint64_t transpose8x8(uint64_t x) {
 }
 
 // ---- wave64 / block scans --------------------------------------------------
+// Wave scans run on DPP lane moves (VALU, no LDS round trip): row_shr:1,2,4,8
+// scan each 16-lane row, row_bcast:15 / row_bcast:31 carry rows 0->1, 2->3
+// and 0-1 -> 2-3.  Lanes with no source read 0 (old = 0, bound_ctrl).
+enum : int {
+  DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118,
+  DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143
+};
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint64_t dpp0(uint64_t v) {
+  return (uint64_t)dpp0<CTRL, ROWS>((uint32_t)v) | ((uint64_t)dpp0<CTRL, ROWS>((uint32_t)(v >> 32)) << 32);
+}
+// the six steps; the bcast steps write only the rows named (0xa: rows 1, 3;
+// 0xc: rows 2, 3), every other lane reads 0
+template <class T, class F>
+__device__ __forceinline__ void wave_scan_steps(T& x, F&& comb) {
+  comb(dpp0<DPP_ROW_SHR1>(x), 1);
+  comb(dpp0<DPP_ROW_SHR2>(x), 2);
+  comb(dpp0<DPP_ROW_SHR4>(x), 4);
+  comb(dpp0<DPP_ROW_SHR8>(x), 8);
+  comb(dpp0<DPP_ROW_BCAST15, 0xa>(x), 15);
+  comb(dpp0<DPP_ROW_BCAST31, 0xc>(x), 31);
+}
+
 __device__ __forceinline__ uint64_t wave_incscan_u64(uint64_t x) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
+  wave_scan_steps(x, [&](uint64_t y, int) { x += y; });
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_incscan_u32(uint32_t x) {
+  wave_scan_steps(x, [&](uint32_t y, int) { x += y; });
   return x;
 }
 

@@ -46,7 +46,16 @@ struct FastLds {
 
 struct View {
   uint32_t base, n;  // bytes [base, base+n) of L.X
+  // 1: base == 0 and dword D of the view lies at dword swz_dw(D) of L.X
+  // (written by DD for a following 4-byte byteshuffle only)
+  uint32_t swz;
 };
+
+// Bank swizzle of a DD output slice (32 dwords per thread): the thread's 16-B
+// units rotate by (slice & 7), so a wave's slice stores and the byteshuffle's
+// plane reads are both conflict-free.  An involution within each 256-dword
+// block.
+__device__ __forceinline__ uint32_t swz_dw(uint32_t d) { return d ^ (((d >> 5) & 7u) << 2); }
 
 // Thread index, opaque to the optimizer: the per-thread index math of the
 // unrolled stage loops is tile-invariant, and hoisting it out of the
@@ -247,13 +256,25 @@ __device__ __forceinline__ void drive2(FastLds& L, uint32_t n, uint32_t nfast, b
   // u = tid + k*FNT, lane-consecutive, so LDS reads and writes are
   // conflict-free), barrier, then written back to X[0, n)
   constexpr int NU = (XCAP + UB * FNT - 1) / (UB * FNT);
+  constexpr int RI = UB == 16 ? 4 : 1;  // units per straight-line batch
   uint32_t r[NU * UD];
 #pragma unroll
-  for (int k = 0; k < NU; k++) {
-    const uint32_t u = t + k * FNT;
-    if (u < nfast) ffast(u, *(uint32_t(*)[UD])(r + k * UD));
-    else if (u * UB < n) fany(u, *(uint32_t(*)[UD])(r + k * UD));
-    if (k % RU == RU - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
+  for (int k0 = 0; k0 < NU; k0 += RI) {
+    const int kend = k0 + RI < NU ? k0 + RI : NU;
+    if ((uint32_t)kend * FNT <= nfast) {
+      // every unit of the batch takes the fast form (uniform): no per-unit
+      // control flow, so the batch's LDS reads issue together
+#pragma unroll
+      for (int k = k0; k < kend; k++) ffast(t + k * FNT, *(uint32_t(*)[UD])(r + k * UD));
+    } else {
+#pragma unroll
+      for (int k = k0; k < kend; k++) {
+        const uint32_t u = t + k * FNT;
+        if (u < nfast) ffast(u, *(uint32_t(*)[UD])(r + k * UD));
+        else if (u * UB < n) fany(u, *(uint32_t(*)[UD])(r + k * UD));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
   }
   __syncthreads();
 #pragma unroll
@@ -333,13 +354,36 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
       w[d] = v;
     }
   };
-  if (TS == 4) {
+  if (TS == 4 && (cur.swz || ((base & 3) == 0 && (N & 3) == 0))) {
+    // planes start on dword boundaries: one dword per plane per unit
+    const uint32_t swz = cur.swz, q = N >> 2;
+    auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
+      uint32_t p[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t d = k * q + u;
+        p[k] = *(const uint32_t*)(X + base + 4 * (swz ? swz_dw(d) : d));
+      }
+      const uint32_t a = __builtin_amdgcn_perm(p[1], p[0], 0x05010400u);
+      const uint32_t b = __builtin_amdgcn_perm(p[3], p[2], 0x05010400u);
+      const uint32_t c = __builtin_amdgcn_perm(p[1], p[0], 0x07030602u);
+      const uint32_t d = __builtin_amdgcn_perm(p[3], p[2], 0x07030602u);
+      w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+      w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+      w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
+    };
+    // (swz implies n = 4N with N % 4 == 0: every unit is a fast unit)
+    drive2<16>(L, n, full / 16, final, gout, fast, [&](uint32_t u, uint32_t (&w)[4]) {
+      if (16 * u + 16 <= full) fast(u, w);
+      else slow(u, w);
+    });
+  } else if (TS == 4) {
     auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
       const uint32_t i = 4 * u;
       // the four plane reads issued together, aligned afterwards
       const uint32_t o0 = base + i, o1 = o0 + N, o2 = o1 + N, o3 = o2 + N;
       const uint2 r0 = lds_pair(X, o0), r1 = lds_pair(X, o1), r2 = lds_pair(X, o2), r3 = lds_pair(X, o3);
-      __builtin_amdgcn_sched_barrier(0);
       const uint32_t p0 = __builtin_amdgcn_alignbyte(r0.y, r0.x, o0 & 3);
       const uint32_t p1 = __builtin_amdgcn_alignbyte(r1.y, r1.x, o1 & 3);
       const uint32_t p2 = __builtin_amdgcn_alignbyte(r2.y, r2.x, o2 & 3);
@@ -403,6 +447,7 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
   }
   cur.base = 0;
   cur.n = n;
+  cur.swz = 0;
   return true;
 }
 
@@ -479,9 +524,9 @@ __device__ __forceinline__ uint64_t bwr_elem(const uint8_t* X, uint32_t base, ui
   return v + (((uint64_t)e.w << 32) | e.z);
 }
 
-template <int W, bool SGN>
+template <int W, bool SGN, class M>
 __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
-                      uint8_t* gout, uint32_t cap, uint32_t dts, uint32_t pos) {
+                      uint8_t* gout, uint32_t cap, uint32_t dts, uint32_t pos, M&& mark) {
   const uint32_t tid = tid_();
   if (mn < 8) return false;
   const uint32_t orig = lds32(L.MD, mo), nw = lds32(L.MD, mo + 4);
@@ -566,6 +611,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     L.TAB[tid] = ent;
   }
   __syncthreads();
+  mark(6);  // TEMP diagnostics
   const uint8_t* X = L.X;
   const uint32_t base = cur.base;
   const bool pow2 = (ws0 & (ws0 - 1)) == 0;
@@ -589,7 +635,6 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
       uint32_t d[5];
 #pragma unroll
       for (int k = 0; k < 5; k++) d[k] = *(const uint32_t*)(X + a + 4 * k);
-      __builtin_amdgcn_sched_barrier(0);
       uint32_t q[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -634,7 +679,6 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
       uint32_t d[5];
 #pragma unroll
       for (int k = 0; k < 5; k++) d[k] = *(const uint32_t*)(X + a + 4 * k);
-      __builtin_amdgcn_sched_barrier(0);
       uint32_t q[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -744,14 +788,20 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
 // last head).  Exclusive scan; returns the carry into this thread's slice.
 __device__ __forceinline__ uint64_t block_segscan(bool has, uint64_t sum, uint64_t* red) {
   const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
+  // (has head, sum since the last head) inclusive over the wave with DPP
+  // moves (a lane with no source reads (0, 0), the identity)
   uint32_t ih = has;
   uint64_t is = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t oh = __shfl_up(ih, d, 64);
-    const uint64_t os = __shfl_up(is, d, 64);
-    if (lane >= (uint32_t)d && !ih) { is = os + is; ih = oh; }
-  }
+  auto comb = [&](uint32_t oh, uint64_t os) {
+    if (!ih) { is = os + is; ih = oh; }
+  };
+  comb(dpp0<DPP_ROW_SHR1>(ih), dpp0<DPP_ROW_SHR1>(is));
+  comb(dpp0<DPP_ROW_SHR2>(ih), dpp0<DPP_ROW_SHR2>(is));
+  comb(dpp0<DPP_ROW_SHR4>(ih), dpp0<DPP_ROW_SHR4>(is));
+  comb(dpp0<DPP_ROW_SHR8>(ih), dpp0<DPP_ROW_SHR8>(is));
+  comb(dpp0<DPP_ROW_BCAST15, 0xa>(ih), dpp0<DPP_ROW_BCAST15, 0xa>(is));
+  comb(dpp0<DPP_ROW_BCAST31, 0xc>(ih), dpp0<DPP_ROW_BCAST31, 0xc>(is));
+  // exclusive = the inclusive value of lane - 1
   uint32_t eh = __shfl_up(ih, 1, 64);
   uint64_t es = __shfl_up(is, 1, 64);
   if (lane == 0) { eh = 0; es = 0; }
@@ -964,16 +1014,21 @@ template <class U>
 __device__ __forceinline__ void block_ddscan_u(U& E, U& Xs, uint32_t cnt, U* red) {
   const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
   U iE = E, iX = Xs;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const U oE = __shfl_up(iE, d, 64), oX = __shfl_up(iX, d, 64);
-    if (lane >= (uint32_t)d) {
-      iX = oX + iX + (U)d * (U)cnt * oE;
-      iE = oE + iE;
-    }
-  }
-  U eE = __shfl_up(iE, 1, 64), eX = __shfl_up(iX, 1, 64);
-  if (lane == 0) { eE = 0; eX = 0; }
+  // DPP steps: the received segment precedes this lane's own segment of
+  // `len` lanes (row_shr:d: d lanes; bcast15 into rows 1, 3: lane%32 - 15;
+  // bcast31 into rows 2, 3: lane - 31); a lane with no source reads (0, 0)
+  auto comb = [&](U oE, U oX, uint32_t len) {
+    iX = oX + iX + (U)len * (U)cnt * oE;
+    iE = oE + iE;
+  };
+  comb(dpp0<DPP_ROW_SHR1>(iE), dpp0<DPP_ROW_SHR1>(iX), 1);
+  comb(dpp0<DPP_ROW_SHR2>(iE), dpp0<DPP_ROW_SHR2>(iX), 2);
+  comb(dpp0<DPP_ROW_SHR4>(iE), dpp0<DPP_ROW_SHR4>(iX), 4);
+  comb(dpp0<DPP_ROW_SHR8>(iE), dpp0<DPP_ROW_SHR8>(iX), 8);
+  comb(dpp0<DPP_ROW_BCAST15, 0xa>(iE), dpp0<DPP_ROW_BCAST15, 0xa>(iX), (lane & 31) - 15);
+  comb(dpp0<DPP_ROW_BCAST31, 0xc>(iE), dpp0<DPP_ROW_BCAST31, 0xc>(iX), lane - 31);
+  // exclusive from inclusive: iX = eX + X_own + cnt * eE (own = 1 lane)
+  const U eE = iE - E, eX = iX - Xs - (U)cnt * eE;
   if (lane == 63) { red[2 * wid] = iE; red[2 * wid + 1] = iX; }
   __syncthreads();
   U PE = 0, PX = 0;
@@ -1207,12 +1262,127 @@ __device__ __forceinline__ void dd_decode_part32(FastLds& L, uint32_t src, uint3
   __syncthreads();
 }
 
-template <int W, class M>
-__device__ __forceinline__ void dd_decode_part(FastLds& L, uint32_t src, uint32_t b, uint64_t num,
+// DoubleDelta data part for 32-bit values, code width CB = bitsize + 1 known
+// at compile time.  Thread t owns codes [32t, 32t + 32): exactly the 32-bit
+// MSB-first stream chunks [t CB, t CB + CB), so every code's chunk index and
+// bit offset inside the thread's chunk window are constants.  The window is
+// read straight from the BWR / load output (CB + 3 aligned dwords, byte-
+// realigned with one alignbyte each; chunk 2k of the stream is the HIGH dword
+// of little-endian word k, so chunk k of the window is stream dword
+// (p + k) ^ 1 with p = t CB & 1).  No realignment pass, no per-code LDS read.
+//
+// Codes past the last value (j >= num - 2) decode whatever bits follow the
+// stream; they only reach the aggregates carried into later threads, whose
+// values all lie past num and are never stored.
+template <int CB>
+__device__ __forceinline__ void dd32_codes_cb(const uint8_t* X, uint32_t bs, uint32_t t, uint32_t (&e)[32]) {
+  constexpr int ND = CB + 3;
+  const uint32_t c0 = t * CB;
+  const uint32_t sb = bs + 8 * (c0 >> 1);
+  const uint32_t a = sb & ~3u, sh = sb & 3u;
+  // all-ones when the window starts at an odd chunk; opaque, so the select
+  // below stays a bit-select (a visible p ? M[..] : M[..] becomes a dynamic
+  // index into a scratch copy of M)
+  uint32_t pm = (c0 & 1) ? ~0u : 0u;
+  asm volatile("" : "+v"(pm));
+  uint32_t A[ND];
+#pragma unroll
+  for (int k = 0; k < ND; k++) A[k] = *(const uint32_t*)(X + a + 4 * k);
+  uint32_t M[CB + 2];
+#pragma unroll
+  for (int k = 0; k < CB + 2; k++) M[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+  uint32_t C[CB];
+#pragma unroll
+  for (int k = 0; k < CB; k++) C[k] = (M[(k + 1) ^ 1] & pm) | (M[k ^ 1] & ~pm);
+#pragma unroll
+  for (int q = 0; q < 32; q++) {
+    constexpr int B = CB - 1;
+    const int P = q * CB, k = P >> 5, r = P & 31;
+    // sign = top bit of the code, bit 31 - r of chunk k
+    const uint32_t sg = (uint32_t)__builtin_amdgcn_sbfe((int32_t)C[k], 31 - r, 1);
+    uint32_t mag;
+    if (r + CB <= 32) {
+      mag = B ? __builtin_amdgcn_ubfe(C[k], 32 - r - CB, B) : 0u;
+    } else {
+      const uint32_t z = __builtin_amdgcn_alignbit(C[k], C[k + 1], 64 - r - CB);
+      mag = z & ((1u << B) - 1);
+    }
+    e[q] = (mag ^ sg) - sg;
+  }
+}
+
+// reads of the thread windows stay inside L.X for every thread of the block
+__device__ __forceinline__ bool dd32_fast_ok(uint32_t bs, uint32_t cb) {
+  return cb >= 2 && cb <= 32 && bs + 8 * (((FNT - 1) * cb) >> 1) + 4 * (cb + 3) + 4 <= XCAP;
+}
+
+template <bool SWZ, class M>
+__device__ __forceinline__ bool dd_decode_part32_cb(FastLds& L, uint32_t src, uint32_t b, uint32_t num,
+                                                    M&& mark) {
+  typedef uint32_t U;
+  const uint8_t* X = L.X;
+  const U x0 = lds32(X, src + 9), x1 = lds32(X, src + 13);
+  const uint32_t bs = src + 17;
+  const uint32_t t = tid_();
+  U e[32];
+  switch (b + 1) {
+#define TDBG_DDCB(n) \
+    case n: dd32_codes_cb<n>(X, bs, t, e); break;
+    TDBG_DDCB(2) TDBG_DDCB(3) TDBG_DDCB(4) TDBG_DDCB(5) TDBG_DDCB(6) TDBG_DDCB(7) TDBG_DDCB(8)
+    TDBG_DDCB(9) TDBG_DDCB(10) TDBG_DDCB(11) TDBG_DDCB(12) TDBG_DDCB(13) TDBG_DDCB(14) TDBG_DDCB(15)
+    TDBG_DDCB(16) TDBG_DDCB(17) TDBG_DDCB(18) TDBG_DDCB(19) TDBG_DDCB(20) TDBG_DDCB(21) TDBG_DDCB(22)
+    TDBG_DDCB(23) TDBG_DDCB(24) TDBG_DDCB(25) TDBG_DDCB(26) TDBG_DDCB(27) TDBG_DDCB(28) TDBG_DDCB(29)
+    TDBG_DDCB(30) TDBG_DDCB(31)
+    default: dd32_codes_cb<32>(X, bs, t, e); break;
+#undef TDBG_DDCB
+  }
+  U E = 0, Xs = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    E += e[k];
+    Xs += E;
+  }
+  block_ddscan_u<U>(E, Xs, 32, (U*)L.red);
+  mark(7);  // diagnostics: code reads + scan
+  // state after codes [0, 32t): d_{32t+1}, x_{32t+1}
+  const U d1 = x1 - x0;
+  U d = d1 + E;
+  U x = x1 + (U)(32 * t) * d1 + Xs;
+  U v[32];
+  v[0] = x - d;
+  v[1] = x;
+#pragma unroll
+  for (int k = 2; k < 32; k++) {
+    d += e[k - 2];
+    x += d;
+    v[k] = x;
+  }
+  __syncthreads();  // every stream read before the values overwrite it
+  // swizzled layout for a following 4-byte byteshuffle (its planes then
+  // start on 16-B unit boundaries: num % 4 == 0)
+  const bool swz = SWZ && (num & 3) == 0;
+  {
+    const uint32_t s0 = t * SP, n = num * 4, rot = swz ? (t & 7) : 0u;
+#pragma unroll
+    for (int q = 0; q < SP / 16; q++) {
+      const uint32_t o = s0 + 16 * q;
+      if (o < n)
+        *(uint4*)(L.X + s0 + 16 * (q ^ rot)) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+  }
+  __syncthreads();
+  return swz;
+}
+
+// returns true when the output was written in the swz_dw layout
+template <int W, bool SWZ, class M>
+__device__ __forceinline__ bool dd_decode_part(FastLds& L, uint32_t src, uint32_t b, uint64_t num,
                                                M&& mark) {
+  if (W == 4 && dd32_fast_ok(src + 17, b + 1)) return dd_decode_part32_cb<SWZ>(L, src, b, (uint32_t)num, mark);
   if (W == 4) dd_decode_part32(L, src, b, (uint32_t)num, mark);
   else if (((src + 9 + 2 * W) & 3) == 0) dd_decode_part_t<W, true>(L, src, b, (uint32_t)num, mark);
   else dd_decode_part_t<W, false>(L, src, b, (uint32_t)num, mark);
+  return false;
 }
 
 // ---------------------------------------------------------------------------
@@ -1246,7 +1416,7 @@ __device__ bool comp_header(FastLds& L, View cur, uint32_t mo, uint32_t mn, uint
   return p <= cur.n && md_total <= MDCAP;
 }
 
-template <int W, class M>
+template <int W, bool SWZ, class M>
 __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap, M&& mark) {
   // compression md header (compression_filter.cc:323-347) from a wave
@@ -1336,9 +1506,10 @@ __device__ __forceinline__ bool f_dd(FastLds& L, View& cur, uint32_t& mo, uint32
     return true;
   }
   mark(4);  // diagnostics: DD header + metadata parts
-  dd_decode_part<W>(L, cur.base + src, b, num, mark);
+  const bool swz = dd_decode_part<W, SWZ>(L, cur.base + src, b, num, mark);
   cur.base = 0;
   cur.n = u;
+  cur.swz = swz ? 1u : 0u;
   if (final) final_copy(L, cur, gout);
   return true;
 }
@@ -1416,7 +1587,7 @@ __device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint3
 // inference see one small straight-line program.
 #define SC(kind, w, sg) ((kind) | ((w) << 4) | ((sg) << 8))
 
-template <int CODE, int POS, class M>
+template <int CODE, int POS, int NEXT, class M>
 __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn,
                                           bool final, uint8_t* gout, uint32_t cap,
                                           const tdbg_stage& s, M&& mark) {
@@ -1433,11 +1604,13 @@ __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, u
   } else if constexpr (K == TDBG_K_BITSHUFFLE) {
     return f_bitshuffle<W>(L, cur, mo, mn, final, gout, cap);
   } else if constexpr (K == TDBG_K_BWR) {
-    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts, POS);
+    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts, POS, mark);
   } else if constexpr (K == TDBG_K_PD) {
     return f_pd<W>(L, cur, mo, mn, final, gout, cap, s.dts);
   } else if constexpr (K == TDBG_K_DD) {
-    return f_dd<W>(L, cur, mo, mn, final, gout, cap, mark);
+    // the next stage (the one run after this) is a 4-byte byteshuffle
+    constexpr bool SWZ = NEXT == SC(TDBG_K_BYTESHUFFLE, 4, 0);
+    return f_dd<W, SWZ>(L, cur, mo, mn, final, gout, cap, mark);
   } else if constexpr (K == TDBG_K_RLE) {
     return f_rle(L, cur, mo, mn, final, gout, cap, (uint32_t)s.cs);
   } else {
@@ -1482,25 +1655,25 @@ __device__ __forceinline__ bool f_resident(const tdbg_plan& P, View cur, uint32_
   // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
   if constexpr (S3 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
-    if (!run_stage<S3, 3>(L, cur, mo, mn, false, gout, orig, P.s[3], mark)) return false;
+    if (!run_stage<S3, 3, S2>(L, cur, mo, mn, false, gout, orig, P.s[3], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(2);
   }
   if constexpr (S2 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S2, 2>(L, cur, mo, mn, false, gout, orig, P.s[2], mark)) return false;
+    if (!run_stage<S2, 2, (S1 != 0 ? S1 : S0)>(L, cur, mo, mn, false, gout, orig, P.s[2], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 3 : 2);
   }
   if constexpr (S1 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S1, 1>(L, cur, mo, mn, false, gout, orig, P.s[1], mark)) return false;
+    if (!run_stage<S1, 1, S0>(L, cur, mo, mn, false, gout, orig, P.s[1], mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 4 : S2 != 0 ? 3 : 2);
   }
   if (dbg_stop > 1) return true;
   hook();
-  const bool ok = run_stage<S0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0], mark);
+  const bool ok = run_stage<S0, 0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0], mark);
   mark(5);
   return ok;
 }
