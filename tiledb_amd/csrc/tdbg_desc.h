@@ -43,7 +43,7 @@ struct tdbg_plan {
 };
 
 #define TDBG_E_FALLBACK 100  // internal status: the fast path declined the tile
-#define TDBG_PROF_PHASES 8  // fused-kernel phase clocks per workgroup
+#define TDBG_PROF_PHASES 16 // fused-kernel phase clocks per workgroup
 
 enum tdbg_fast_kind : uint32_t {
   TDBG_FAST_NONE = 0,

@@ -357,13 +357,7 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
   if (TS == 4 && (cur.swz || ((base & 3) == 0 && (N & 3) == 0))) {
     // planes start on dword boundaries: one dword per plane per unit
     const uint32_t swz = cur.swz, q = N >> 2;
-    auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
-      uint32_t p[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t d = k * q + u;
-        p[k] = *(const uint32_t*)(X + base + 4 * (swz ? swz_dw(d) : d));
-      }
+    auto unit = [&](const uint32_t (&p)[4], uint32_t (&w)[4]) {
       const uint32_t a = __builtin_amdgcn_perm(p[1], p[0], 0x05010400u);
       const uint32_t b = __builtin_amdgcn_perm(p[3], p[2], 0x05010400u);
       const uint32_t c = __builtin_amdgcn_perm(p[1], p[0], 0x07030602u);
@@ -373,11 +367,32 @@ __device__ __forceinline__ bool f_byteshuffle(FastLds& L, View& cur, uint32_t& m
       w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
       w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
     };
-    // (swz implies n = 4N with N % 4 == 0: every unit is a fast unit)
-    drive2<16>(L, n, full / 16, final, gout, fast, [&](uint32_t u, uint32_t (&w)[4]) {
+    auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
+      uint32_t p[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t d = k * q + u;
+        p[k] = *(const uint32_t*)(X + base + 4 * (swz ? swz_dw(d) : d));
+      }
+      unit(p, w);
+    };
+    auto slowu = [&](uint32_t u, uint32_t (&w)[4]) {
       if (16 * u + 16 <= full) fast(u, w);
       else slow(u, w);
-    });
+    };
+    if (base == 0 && N == 16384) {
+      // a 64 KiB chunk: plane k starts at byte 16384 k (a multiple of the
+      // swizzle block), so one address + immediate offsets reads all planes
+      auto fast64 = [&](uint32_t u, uint32_t (&w)[4]) {
+        const uint32_t* P = (const uint32_t*)(X + 4 * (swz ? swz_dw(u) : u));
+        const uint32_t p[4] = {P[0], P[4096], P[8192], P[12288]};
+        unit(p, w);
+      };
+      drive2<16>(L, n, full / 16, final, gout, fast64, slowu);
+    } else {
+      // (swz implies n = 4N with N % 4 == 0: every unit is a fast unit)
+      drive2<16>(L, n, full / 16, final, gout, fast, slowu);
+    }
   } else if (TS == 4) {
     auto fast = [&](uint32_t u, uint32_t (&w)[4]) {
       const uint32_t i = 4 * u;
@@ -535,32 +550,12 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
   if (final ? orig > cap : orig > XCAP) return false;
   const uint32_t ws0 = lds32(L.MD, mo + 8 + dts + 1);
   bool bad = ws0 == 0 || ws0 % W != 0;
-  {
-    // Wave-local identity test (no barrier): every wave checks all windows.
-    // All windows raw with the uniform window layout <=> each window is
-    // copied to its own offset, and the stage is the identity on the first
-    // orig bytes (the common case for incompressible data).
-    const uint32_t lane = tid & 63;
-    bool nonraw = false, badl = false;
-    for (uint32_t w0 = 0; w0 < nw; w0 += 64) {
-      const uint32_t w = w0 + lane;
-      if (w < nw) {
-        const uint32_t eo = mo + 8 + w * E;
-        const uint32_t bits = L.MD[eo + dts], nbw = lds32(L.MD, eo + dts + 1);
-        nonraw |= !(bits >= 8u * W || (nbw % W) != 0);
-        badl |= w + 1 < nw ? nbw != ws0 : (nbw == 0 || nbw > ws0);
-      }
-    }
-    if (!bad && __ballot(nonraw) == 0 && __ballot(badl) == 0) {
-      const uint64_t tot = (uint64_t)(nw - 1) * ws0 + lds32(L.MD, mo + 8 + (nw - 1) * E + dts + 1);
-      if (tot != orig || tot > cur.n) return false;
-      mo += 8 + nw * E;
-      mn -= 8 + nw * E;
-      cur.n = orig;
-      if (final) final_copy(L, cur, gout);
-      return true;
-    }
-  }
+  // One pass over the windows (thread w owns window w): its entry, a DPP
+  // wave scan of (compressed bytes, bytes) packed in a u64 (both sums
+  // < 2^32) with the 'bad' / 'not raw' flags alongside, and its table entry
+  // with the wave-local input offset -- all before the stage's single
+  // barrier.  Readers add the exclusive prefix of the window's wave.  Every
+  // window raw <=> the stage is the identity on the first orig bytes.
   uint32_t comp = 0, nb = 0;
   uint4 ent = make_uint4(0, 0, 0, 0);
   if (tid < nw) {
@@ -575,28 +570,30 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     if (nb > XCAP) bad = true;  // keeps the packed sums below 2^32
     ent = make_uint4(0, bits | (raw ? 0x100u : 0u), (uint32_t)off, (uint32_t)(off >> 32));
   }
-  // one scan of (comp, nb) packed in a u64 (both sums < 2^32), with the
-  // 'bad' and 'not raw' flags OR-ed alongside: a single barrier.  Every
-  // window raw <=> in_off == tid * ws0 (non-last windows hold ws0 bytes), in
-  // which case the stage is the identity on the first orig bytes.
   const uint32_t lane = tid & 63, wid = tid >> 6;
   const uint64_t packed = ((uint64_t)comp << 32) | nb;
   const uint64_t inc = wave_incscan_u64(packed);
   const bool badw = __ballot(bad) != 0;
   const bool cmpw = __ballot(tid < nw && !(ent.y & 0x100u)) != 0;
+  if (tid < nw) {
+    ent.x = (uint32_t)((inc - packed) >> 32);
+    L.TAB[tid] = ent;
+  }
   if (lane == 63) L.scan2[pos & 1][wid] = inc;
   if (lane == 0) L.scanf[pos & 1][wid] = (badw ? 1u : 0u) | (cmpw ? 2u : 0u);
   __syncthreads();
-  uint64_t pre = 0, tot = 0;
+  static_assert(FNT / 64 == 8, "wave prefixes below assume 8 waves");
+  uint64_t tot = 0;
   uint32_t fl = 0;
-#pragma unroll
-  for (int i = 0; i < FNT / 64; i++) {
-    const uint64_t s = L.scan2[pos & 1][i];
-    if ((uint32_t)i < wid) pre += s;
-    tot += s;
-    fl |= L.scanf[pos & 1][i];
-  }
-  const uint32_t in_off = (uint32_t)((pre + inc - packed) >> 32);
+  // exclusive input-offset prefix of each wave, as separate values (an
+  // array indexed by the window's wave would be demoted to scratch)
+  uint32_t P0, P1, P2, P3, P4, P5, P6, P7;
+#define TDBG_WPRE(i)                                              \
+  P##i = __builtin_amdgcn_readfirstlane((uint32_t)(tot >> 32));   \
+  tot += L.scan2[pos & 1][i];                                     \
+  fl |= L.scanf[pos & 1][i];
+  TDBG_WPRE(0) TDBG_WPRE(1) TDBG_WPRE(2) TDBG_WPRE(3) TDBG_WPRE(4) TDBG_WPRE(5) TDBG_WPRE(6) TDBG_WPRE(7)
+#undef TDBG_WPRE
   const uint64_t tin = tot >> 32, tout = tot & 0xffffffffu;
   if ((fl & 1u) || tin > cur.n || tout != orig) return false;
   mo += 8 + nw * E;
@@ -606,11 +603,29 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     if (final) final_copy(L, cur, gout);
     return true;
   }
-  if (tid < nw) {
-    ent.x = in_off;
-    L.TAB[tid] = ent;
-  }
-  __syncthreads();
+  // the input offset of window w: its wave-local offset + its wave's prefix
+  auto wpre = [&](uint32_t w) -> uint32_t {
+    const uint32_t i = w >> 6;
+    const uint32_t a0 = (i & 1) ? P1 : P0, a1 = (i & 1) ? P3 : P2;
+    const uint32_t a2 = (i & 1) ? P5 : P4, a3 = (i & 1) ? P7 : P6;
+    const uint32_t b0 = (i & 2) ? a1 : a0, b1 = (i & 2) ? a3 : a2;
+    return (i & 4) ? b1 : b0;
+  };
+  auto tab = [&](uint32_t w) -> uint4 {
+    uint4 e = L.TAB[w];
+    e.x += wpre(w);
+    return e;
+  };
+  // Power-of-two windows of >= 128 B: the units one call of the fast unit
+  // function covers (u = t + k FNT, t < 512) all lie in windows of one wave
+  // (w >> 6 = u >> (log2 ws0 + 2) >= 9 bits), so the prefix is picked with
+  // scalar selects.  (Clamped units of a final round may differ; their
+  // results are discarded.)
+  auto tab_u = [&](uint32_t w) -> uint4 {
+    uint4 e = L.TAB[w];
+    e.x += wpre(__builtin_amdgcn_readfirstlane(w));
+    return e;
+  };
   mark(6);  // TEMP diagnostics
   const uint8_t* X = L.X;
   const uint32_t base = cur.base;
@@ -620,13 +635,14 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     const uint32_t w = pow2 ? (o >> wsh) : (o / ws0);
     return w < nw ? w : nw - 1;
   };
+  const bool wuni = pow2 && wsh >= 7;
   if (W == 4 && ws0 % 16 == 0) {
     // 32-bit values: compressed widths are 8 or 16 bits (32 is raw), so a
     // 16-B output unit = 4 elements from <= 8 source bytes (q0, q1) with
     // 32-bit bit-field extracts; raw units take the 16 bytes as they are.
-    auto fn16w4 = [&](uint32_t u, uint32_t (&wv)[4]) {
+    auto fn16w4g = [&](uint32_t u, uint32_t (&wv)[4], auto&& tabf) {
       const uint32_t o = 16 * u, w = win(o);
-      const uint4 e = L.TAB[w];
+      const uint4 e = tabf(w);
       const uint32_t ob = o - w * ws0;
       const bool raw = (e.y & 0x100u) != 0;
       const uint32_t bits = e.y & 0xf8u;  // 8 * compressed bytes
@@ -647,13 +663,15 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         wv[k] = raw ? q[k] : v + e.z;
       }
     };
-    drive2<16>(L, orig, orig / 16, final, gout, fn16w4, [&](uint32_t u, uint32_t (&wv)[4]) {
+    auto fn16w4 = [&](uint32_t u, uint32_t (&wv)[4]) { fn16w4g(u, wv, tab); };
+    auto fn16w4u = [&](uint32_t u, uint32_t (&wv)[4]) { fn16w4g(u, wv, tab_u); };
+    auto part4 = [&](uint32_t u, uint32_t (&wv)[4]) {
       // partial last unit: element-wise (the window may hold fewer bytes)
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) {
         const uint32_t o = 16 * u + 4 * k;
         const uint32_t w = win(o);
-        const uint4 e = L.TAB[w];
+        const uint4 e = tab(w);
         const uint32_t ob = o - w * ws0;
         uint64_t v = 0;
         if (o < orig) {
@@ -662,7 +680,9 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         }
         wv[k] = (uint32_t)v;
       }
-    });
+    };
+    if (wuni) drive2<16>(L, orig, orig / 16, final, gout, fn16w4u, part4);
+    else drive2<16>(L, orig, orig / 16, final, gout, fn16w4, part4);
   } else if ((W == 4 || W == 8) && ws0 % 16 == 0) {
     // Every 16-B output unit lies in one window: one TAB read per unit, the
     // unit's source bytes read as one aligned span, elements extracted in
@@ -670,7 +690,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     constexpr uint32_t NE = 16 / W;
     auto fn16 = [&](uint32_t u, uint32_t (&wv)[4]) {
       const uint32_t o = 16 * u, w = win(o);
-      const uint4 e = L.TAB[w];
+      const uint4 e = tab(w);
       const uint32_t ob = o - w * ws0;
       const bool raw = (e.y & 0x100u) != 0;
       const uint32_t cb = (e.y & 0xffu) >> 3;
@@ -710,7 +730,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
       for (uint32_t k = 0; k < NE; k++) {
         const uint32_t o = 16 * u + W * k;
         const uint32_t w = win(o);
-        const uint4 e = L.TAB[w];
+        const uint4 e = tab(w);
         const uint32_t ob = o - w * ws0;
         uint64_t v = 0;
         if (o < orig) {
@@ -731,7 +751,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
       for (int h = 0; h < 2; h++) {
         const uint32_t o = 16 * u + 8 * h;
         const uint32_t w = win(o);
-        const uint4 e = L.TAB[w];
+        const uint4 e = tab(w);
         const uint32_t ob = o - w * ws0;
         uint64_t v;
         if (e.y & 0x100u) v = lds64(X, base + e.x + ob);
@@ -744,12 +764,12 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
   } else if (W == 4) {
     auto fn = [&](uint32_t u, uint32_t (&wv)[4]) {
       uint32_t w = win(16 * u);
-      uint4 e = L.TAB[w];
+      uint4 e = tab(w);
 #pragma unroll
       for (int d = 0; d < 4; d++) {
         const uint32_t o = 16 * u + 4 * d;
         const uint32_t w2 = win(o);
-        if (w2 != w) { w = w2; e = L.TAB[w]; }
+        if (w2 != w) { w = w2; e = tab(w); }
         const uint32_t ob = o - w * ws0;
         if (e.y & 0x100u) wv[d] = lds32(X, base + e.x + ob);
         else wv[d] = (uint32_t)bwr_elem<W, SGN>(X, base, e, ob >> 2);
@@ -765,7 +785,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         for (int h = 0; h < 2; h++) {
           const uint32_t o = 16 * u + 4 * d + 2 * h;
           const uint32_t w = win(o);
-          const uint4 e = L.TAB[w];
+          const uint4 e = tab(w);
           const uint32_t ob = o - w * ws0;
           uint32_t x;
           if (e.y & 0x100u) x = lds32(X, base + e.x + ob) & 0xffffu;

@@ -10,7 +10,8 @@ import bench
 import workloads as W
 from tiledb_amd import engine
 
-NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c|dd-hdr", "final", "tail", "dd-codes+scan"]
+NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c|dd-hdr", "final", "tail", "dd-codes+scan",
+         "p8", "p9", "p10", "p11", "p12", "p13", "p14", "p15"]
 _ser, _dt, _cs, _, _ = W.config("c5")
 dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)
@@ -21,7 +22,7 @@ for var in sys.argv[1:] or ["rand", "ramp"]:
         ctx.unfilter_async(dp, batch)
     torch.cuda.synchronize()
     ms = ctx.last_kernel_ms()
-    clk = ctx.phase_clocks().astype(np.float64)
+    clk = ctx.phase_clocks(16).astype(np.float64)
     tot = clk.sum()
     print(f"{var}: launch {ms:.4f} ms; per-WG phase share:",
           ", ".join(f"{n} {100 * c / tot:.1f}%" for n, c in zip(NAMES, clk) if c), flush=True)
