@@ -664,7 +664,35 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
       }
     };
     auto fn16w4 = [&](uint32_t u, uint32_t (&wv)[4]) { fn16w4g(u, wv, tab); };
-    auto fn16w4u = [&](uint32_t u, uint32_t (&wv)[4]) { fn16w4g(u, wv, tab_u); };
+    // power-of-two windows >= 128 B: shifts instead of multiplies, the scalar
+    // prefix pick, and the two compressed widths (8 / 16 bits) as plain
+    // bit-field extracts of q0 / q1
+    auto fn16w4u = [&](uint32_t u, uint32_t (&wv)[4]) {
+      const uint32_t o = 16 * u;
+      uint32_t w = o >> wsh;
+      w = w < nw ? w : nw - 1;
+      const uint4 e = tab_u(w);
+      const uint32_t ob = o - (w << wsh);
+      const bool raw = (e.y & 0x100u) != 0;
+      const uint32_t bits = e.y & 0xf8u;  // 8 or 16 unless raw
+      const uint32_t src = base + e.x + (raw ? ob : ((ob >> 2) << (bits >> 4)));
+      const uint32_t a = src & ~3u, sh = src & 3u;
+      uint32_t d[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) d[k] = *(const uint32_t*)(X + a + 4 * k);
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      const bool w16 = bits > 8;
+      const uint32_t hi = w16 ? q[1] : q[0];
+      const uint32_t f[4][2] = {{q[0], 0u}, {q[0], bits}, {hi, w16 ? 0u : 16u}, {hi, w16 ? 16u : 24u}};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t v = SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)f[k][0], f[k][1], bits)
+                               : __builtin_amdgcn_ubfe(f[k][0], f[k][1], bits);
+        wv[k] = raw ? q[k] : v + e.z;
+      }
+    };
     auto part4 = [&](uint32_t u, uint32_t (&wv)[4]) {
       // partial last unit: element-wise (the window may hold fewer bytes)
 #pragma unroll
@@ -1030,6 +1058,8 @@ __device__ bool rle_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32
 // Double-delta tuple (E, X) exclusive scan in the value width's arithmetic
 // (U = uint32_t for W <= 4: everything is modulo 2^(8W) anyway); cnt
 // elements per thread.
+// (callers issue a barrier before anything else writes `red`: the scan's
+// own trailing barrier is left out)
 template <class U>
 __device__ __forceinline__ void block_ddscan_u(U& E, U& Xs, uint32_t cnt, U* red) {
   const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
@@ -1059,7 +1089,6 @@ __device__ __forceinline__ void block_ddscan_u(U& E, U& Xs, uint32_t cnt, U* red
       PE += red[2 * i];
     }
   }
-  __syncthreads();
   E = PE + eE;
   Xs = PX + eX + (U)lane * (U)cnt * PE;
 }
