@@ -53,13 +53,31 @@ CONFIGS = {
     "c5": dict(tiles_per_gpu=12500, variants="active,rand,ramp", dtype="int32",
                workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
                         "64 KiB tiles (1 chunk), device-resident, 100k tiles / 8 GPUs"),
+    # XOR / DELTA / FLOAT_SCALE pipelines (not BASELINE configs; tiles encoded
+    # on the device by tdbg_filter_tiles, checked against the values)
+    "xor": dict(tiles_per_gpu=10000, variants="sin", dtype="float32",
+                workload="XOR: dense float32, [XOR, BIT_WIDTH_REDUCTION(256)], 10k tiles x 64 KiB"),
+    "delta": dict(tiles_per_gpu=12500, variants="active", dtype="int32",
+                  workload="DELTA: C5's values, [BYTESHUFFLE, DELTA, BIT_WIDTH_REDUCTION(256)], "
+                           "12.5k tiles x 64 KiB"),
+    "fscale": dict(tiles_per_gpu=10000, variants="sin", dtype="float64",
+                   workload="FLOAT_SCALE: dense float64, [FLOAT_SCALE(1e-3, 0, 4 B), "
+                            "BIT_WIDTH_REDUCTION(256)], 10k tiles x 64 KiB"),
 }
 
 
 def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, device: int, seed: int,
-                align: int = 1):
+                align: int = 1, ctx=None, dp=None):
     import workloads as W
-    pool, vals = W.pool(cfg, variant, nunique, seed)
+
+    def encode(vals):
+        st, tiles = ctx.filter(dp, vals)
+        if st.any():
+            raise SystemExit(f"{cfg}: device forward encode failed: {np.unique(st)}")
+        return [t.tobytes() for t in tiles]
+
+    pool, vals = W.pool(cfg, variant, nunique, seed, encode=encode)
+    vals = [W.expected(cfg, v) for v in vals]
     idx = np.arange(ntiles) % nunique
     sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
     offs = engine.pack_offsets(sizes, align)
@@ -284,7 +302,7 @@ def main():
     for vi, var in enumerate(variants):
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
             engine, args.config, var, ntiles, args.unique, local, seed=5 + 1000 * rank + vi,
-            align=args.align)
+            align=args.align, ctx=ctx, dp=dp)
         ablation = bool(os.environ.get("TDBG_DEBUG_STOP"))  # timing-only: outputs unchecked
         st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
         if st.any():
@@ -300,7 +318,7 @@ def main():
         res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
                         out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback,
                         packed=packed, offs=offs, sizes=sizes)
-        if args.forward and vi == 0 and not ablation:
+        if args.forward and vi == 0 and not ablation and args.config != "fscale":  # (lossy: values differ)
             res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, args.steps, args.warmup, dist)
         if args.e2e:
             res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args,
@@ -333,7 +351,8 @@ def main():
         "vs_baseline": None,
         "dtype": cfg["dtype"],
         "data": f"synthetic {args.config.upper()} '{head}' tiles ({args.unique} unique, replicated), "
-                "numpy-encoded (workloads.py)",
+                + ("device-encoded (tdbg_filter_tiles)" if W.config(args.config)[4] is None
+                   else "numpy-encoded (workloads.py)"),
         "config": {
             "workload": cfg["workload"],
             "tiles_per_gpu": ntiles,

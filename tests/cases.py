@@ -454,5 +454,16 @@ def fused_spec_cases(ntiles: int = 3) -> List[Case]:
         Case("spec25_bwr_i32", P(W(256)), I32, 4, tiles(I32) + rand()),
         Case("spec26_bwr_u64", P(W(256)), U64, 8, tiles(U64)),
         Case("spec27_bwr_i64", P(W(256)), I64, 8, tiles(I64) + rand()),
+        # XOR / DELTA / FLOAT_SCALE pipelines
+        Case("spec28_xor_bwr_f32", P(XORFilter(), W(256)), F32, 4, c2_tiles(ntiles)),
+        Case("spec29_xor_bwr_f64", P(XORFilter(), W(256)), F64, 8, f64),
+        Case("spec30_xor_i32", P(XORFilter()), I32, 4, tiles(I32) + rand()),
+        Case("spec31_xor_u64", P(XORFilter()), U64, 8, tiles(U64)),
+        Case("spec32_byte_delta_bwr_i32", P(B(), DELTA(), W(256)), I32, 4, tiles(I32) + rand()),
+        Case("spec33_delta_i32", P(DELTA()), I32, 4, tiles(I32) + rand()),
+        Case("spec34_delta_i64", P(DELTA()), I64, 8, tiles(I64)),
+        Case("spec35_fscale_f64_bw4_bwr", P(FloatScalingFilter(1e-3, 0.0, 4), W(256)), F64, 8, f64),
+        Case("spec36_fscale_f32_bw4", P(FloatScalingFilter(0.125, -3.0, 4)), F32, 4, c2_tiles(ntiles)),
+        Case("spec37_fscale_f64_bw8_bwr", P(FloatScalingFilter(2.0 ** -20, 1.5, 8), W(256)), F64, 8, f64),
     ]
     return out

@@ -56,6 +56,8 @@ struct View {
 // plane reads are both conflict-free.  An involution within each 256-dword
 // block.
 __device__ __forceinline__ uint32_t swz_dw(uint32_t d) { return d ^ (((d >> 5) & 7u) << 2); }
+// the same map on 16-B units: unit U at physical unit U ^ ((U >> 3) & 7)
+__device__ __forceinline__ uint32_t swz_u(uint32_t u) { return u ^ ((u >> 3) & 7u); }
 
 // Thread index, opaque to the optimizer: the per-thread index math of the
 // unrolled stage loops is tile-invariant, and hoisting it out of the
@@ -208,7 +210,7 @@ __device__ __forceinline__ void store_unit(uint8_t* gout, uint32_t n, uint32_t o
 // per-unit control flow); the remaining units use fany.
 template <int UB, class FF, class FA>
 __device__ __forceinline__ void drive2(FastLds& L, uint32_t n, uint32_t nfast, bool final, uint8_t* gout,
-                                       FF ffast, FA fany) {
+                                       FF ffast, FA fany, bool swz_out = false) {
   constexpr int UD = UB / 4;
   constexpr int RU = UB == 16 ? 3 : 1;
   const uint32_t t = tid_();
@@ -284,26 +286,48 @@ __device__ __forceinline__ void drive2(FastLds& L, uint32_t n, uint32_t nfast, b
     for (int q = 0; q < UD / 4; q++) {
       const uint32_t o = u * UB + 16 * q;
       if (o < n)
-        *(uint4*)(L.X + o) = make_uint4(r[k * UD + 4 * q], r[k * UD + 4 * q + 1], r[k * UD + 4 * q + 2],
-                                        r[k * UD + 4 * q + 3]);
+        *(uint4*)(L.X + (swz_out ? 16 * swz_u(o >> 4) : o)) =
+            make_uint4(r[k * UD + 4 * q], r[k * UD + 4 * q + 1], r[k * UD + 4 * q + 2], r[k * UD + 4 * q + 3]);
     }
   }
   __syncthreads();
 }
 
 template <int UB, class F>
-__device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_t* gout, F fn) {
-  drive2<UB>(L, n, 0, final, gout, fn, fn);
+__device__ __forceinline__ void drive(FastLds& L, uint32_t n, bool final, uint8_t* gout, F fn,
+                                      bool swz_out = false) {
+  drive2<UB>(L, n, 0, final, gout, fn, fn, swz_out);
 }
 
 // Copy a view to the final output (pass-through / raw stages as filter 0).
 __device__ void final_copy(FastLds& L, View v, uint8_t* gout) {
+  if (v.swz) {  // base 0, 16-B units swizzled
+    for (uint32_t u = tid_(); u * 16 < v.n; u += FNT)
+      store_unit(gout, v.n, 16 * u, *(const uint4*)(L.X + 16 * swz_u(u)));
+    return;
+  }
   for (uint32_t u = tid_(); u * 16 < v.n; u += FNT) {
     const uint32_t o = v.base + 16 * u;
     uint4 x;
     if ((o & 15) == 0) x = *(const uint4*)(L.X + o);
     else x = make_uint4(lds32(L.X, o), lds32(L.X, o + 4), lds32(L.X, o + 8), lds32(L.X, o + 12));
     store_unit(gout, v.n, 16 * u, x);
+  }
+}
+
+// A thread's 128-B slice [128 t, 128 t + 128) of the view into registers:
+// swizzled views with conflict-free 16-B reads, others dword-wise.
+__device__ __forceinline__ void slice_load(const FastLds& L, const View& v, uint32_t (&r)[SPD]) {
+  const uint32_t t = tid_(), s0 = t * SP;
+  if (v.swz) {
+#pragma unroll
+    for (int q = 0; q < SP / 16; q++) {
+      const uint4 x = *(const uint4*)(L.X + 16 * swz_u(8 * t + q));
+      r[4 * q] = x.x; r[4 * q + 1] = x.y; r[4 * q + 2] = x.z; r[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < SPD; k++) r[k] = (s0 + 4 * k < v.n) ? lds32(L.X, v.base + s0 + 4 * k) : 0u;
   }
 }
 
@@ -539,7 +563,9 @@ __device__ __forceinline__ uint64_t bwr_elem(const uint8_t* X, uint32_t base, ui
   return v + (((uint64_t)e.w << 32) | e.z);
 }
 
-template <int W, bool SGN, class M>
+// SZ: the next stage reads a swizzled view (1: slice stages PD / XOR,
+// 2: a 4-byte byteshuffle, which needs whole 16-B plane units)
+template <int W, bool SGN, int SZ, class M>
 __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                       uint8_t* gout, uint32_t cap, uint32_t dts, uint32_t pos, M&& mark) {
   const uint32_t tid = tid_();
@@ -627,6 +653,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
     return e;
   };
   mark(6);  // TEMP diagnostics
+  const bool so = !final && (SZ == 1 || (SZ == 2 && orig % 16 == 0));
   const uint8_t* X = L.X;
   const uint32_t base = cur.base;
   const bool pow2 = (ws0 & (ws0 - 1)) == 0;
@@ -709,8 +736,8 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         wv[k] = (uint32_t)v;
       }
     };
-    if (wuni) drive2<16>(L, orig, orig / 16, final, gout, fn16w4u, part4);
-    else drive2<16>(L, orig, orig / 16, final, gout, fn16w4, part4);
+    if (wuni) drive2<16>(L, orig, orig / 16, final, gout, fn16w4u, part4, so);
+    else drive2<16>(L, orig, orig / 16, final, gout, fn16w4, part4, so);
   } else if ((W == 4 || W == 8) && ws0 % 16 == 0) {
     // Every 16-B output unit lies in one window: one TAB read per unit, the
     // unit's source bytes read as one aligned span, elements extracted in
@@ -772,7 +799,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
           wv[2 * k + 1] = (uint32_t)(v >> 32);
         }
       }
-    });
+    }, so);
   } else if (W == 8) {
     auto fn = [&](uint32_t u, uint32_t (&wv)[4]) {
 #pragma unroll
@@ -788,7 +815,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         wv[2 * h + 1] = (uint32_t)(v >> 32);
       }
     };
-    drive2<16>(L, orig, orig / 16, final, gout, fn, fn);
+    drive2<16>(L, orig, orig / 16, final, gout, fn, fn, so);
   } else if (W == 4) {
     auto fn = [&](uint32_t u, uint32_t (&wv)[4]) {
       uint32_t w = win(16 * u);
@@ -803,7 +830,7 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         else wv[d] = (uint32_t)bwr_elem<W, SGN>(X, base, e, ob >> 2);
       }
     };
-    drive2<16>(L, orig, orig / 16, final, gout, fn, fn);
+    drive2<16>(L, orig, orig / 16, final, gout, fn, fn, so);
   } else {  // W == 2: two elements per dword, windows may end mid-dword
     drive<16>(L, orig, final, gout, [&](uint32_t u, uint32_t (&wv)[4]) {
 #pragma unroll
@@ -822,10 +849,11 @@ __device__ __forceinline__ bool f_bwr(FastLds& L, View& cur, uint32_t& mo, uint3
         }
         wv[d] = v;
       }
-    });
+    }, so);
   }
   cur.base = 0;
   cur.n = orig;
+  cur.swz = so ? 1u : 0u;
   return true;
 }
 
@@ -887,12 +915,13 @@ __device__ __forceinline__ void rset(uint32_t (&r)[N], int k, uint64_t v) {
 
 // write a slice register file to X[0, n) (after the barrier the caller issues)
 template <int N>
-__device__ __forceinline__ void slice_store(FastLds& L, const uint32_t (&r)[N], uint32_t n) {
-  const uint32_t s0 = tid_() * (4 * N);
+__device__ __forceinline__ void slice_store(FastLds& L, const uint32_t (&r)[N], uint32_t n, bool swz = false) {
+  const uint32_t t = tid_(), s0 = t * (4 * N);
 #pragma unroll
   for (int k = 0; k < N / 4; k++) {
     const uint32_t o = s0 + 16 * k;
-    if (o < n) *(uint4*)(L.X + o) = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+    if (o < n)
+      *(uint4*)(L.X + (swz ? 16 * swz_u(o >> 4) : o)) = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
   }
 }
 
@@ -900,7 +929,7 @@ __device__ __forceinline__ void slice_store(FastLds& L, const uint32_t (&r)[N], 
 // PD^-1 (positive_delta_filter.cc:324-375): segmented prefix sums
 // TAB[w] = {first lo, first hi, nb, raw}
 // ---------------------------------------------------------------------------
-template <int W>
+template <int W, int SZ>
 __device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
                      uint8_t* gout, uint32_t cap, uint32_t dts) {
   const uint32_t tid = tid_();
@@ -927,8 +956,6 @@ __device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32
   mo += 4 + nw * E;
   mn -= 4 + nw * E;
   constexpr int EP = SP / W;  // elements per thread slice
-  const uint8_t* X = L.X;
-  const uint32_t base = cur.base;
   const uint32_t s0 = tid * SP;
   const uint32_t e0 = s0 / W;     // first element of the slice
   const uint32_t epw = ws0 / W;   // elements per (full) window
@@ -936,8 +963,7 @@ __device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32
   // pass 1: the slice's input bytes as dwords (raw-window bytes pass through
   // untouched), deltas, and the segment aggregate (has head, sum after it)
   uint32_t r[SPD];
-#pragma unroll
-  for (int k = 0; k < SPD; k++) r[k] = (s0 + 4 * k < n) ? lds32(X, base + s0 + 4 * k) : 0u;
+  slice_load(L, cur, r);
   // A slice holds at most EP <= epw elements, so it spans at most two
   // windows: w0 (continued from the previous slice unless rem0 == 0) and,
   // from element kh on, w0 + 1.
@@ -973,10 +999,13 @@ __device__ __forceinline__ bool f_pd(FastLds& L, View& cur, uint32_t& mo, uint32
     }
   }
   __syncthreads();
-  slice_store(L, r, n);
+  // swizzled for a slice / byteshuffle consumer (SZ as f_bwr) or the final copy
+  const bool so = final || SZ == 1 || (SZ == 2 && n % 16 == 0);
+  slice_store(L, r, n, so);
   __syncthreads();
   cur.base = 0;
   cur.n = n;
+  cur.swz = so ? 1u : 0u;
   if (final) {
     final_copy(L, cur, gout);
   }
@@ -1628,6 +1657,229 @@ __device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint3
 }
 
 // ---------------------------------------------------------------------------
+// workgroup scans for the slice stages below: inclusive over the block in
+// thread order (DPP within the wave, wave totals through red + one barrier;
+// callers barrier before `red` is written again); returns the exclusive
+// prefix of this thread.  Op: 0 = add, 1 = xor.
+// ---------------------------------------------------------------------------
+template <int OP, class U>
+__device__ __forceinline__ U block_exscan_op(U v, U* red) {
+  const uint32_t lane = tid_() & 63, wid = tid_() >> 6;
+  U inc = v;
+  wave_scan_steps(inc, [&](U y, int) { inc = OP ? (U)(inc ^ y) : (U)(inc + y); });
+  if (lane == 63) red[wid] = inc;
+  __syncthreads();
+  U pre = 0;
+#pragma unroll
+  for (int i = 0; i < FNT / 64; i++)
+    if ((uint32_t)i < wid) pre = OP ? (U)(pre ^ red[i]) : (U)(pre + red[i]);
+  return OP ? (U)(pre ^ inc ^ v) : (U)(pre + inc - v);
+}
+
+// ---------------------------------------------------------------------------
+// XOR^-1 (XORFilter::unxor_part, xor_filter.cc:260-286) for 4- / 8-byte
+// elements: a prefix XOR over the part.  One part covering the view, whole
+// elements only (a tail the reference leaves unwritten declines).  Each
+// thread XOR-scans its 128-B slice in registers; the block scan carries.
+// ---------------------------------------------------------------------------
+template <int W, int SZ>
+__device__ __forceinline__ bool f_xor(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+                                      uint8_t* gout, uint32_t cap) {
+  typedef typename std::conditional<(W == 8), uint64_t, uint32_t>::type U;
+  if (mn < 8) return false;
+  const uint32_t np = lds32(L.MD, mo), ps = lds32(L.MD, mo + 4);
+  if (np != 1 || ps != cur.n || ps % W != 0 || ps > (uint32_t)(FNT * SP)) return false;
+  if (final && ps > cap) return false;
+  mo += 8;
+  mn -= 8;
+  const uint32_t n = ps, base = cur.base, t = tid_();
+  const uint32_t s0 = t * SP;
+  constexpr int EP = SP / W;
+  uint32_t r[SPD];
+  slice_load(L, cur, r);
+  (void)base;
+  (void)s0;
+  U acc = 0;
+#pragma unroll
+  for (int e = 0; e < EP; e++) {
+    acc ^= (U)rget<W>(r, e);
+    rset<W>(r, e, acc);
+  }
+  const U ex = block_exscan_op<1, U>(acc, (U*)L.red);
+#pragma unroll
+  for (int e = 0; e < EP; e++) rset<W>(r, e, (U)rget<W>(r, e) ^ ex);
+  __syncthreads();  // every slice read before the stores
+  const bool so = final || SZ == 1 || (SZ == 2 && n % 16 == 0);
+  slice_store(L, r, n, so);
+  __syncthreads();
+  cur.base = 0;
+  cur.n = n;
+  cur.swz = so ? 1u : 0u;
+  if (final) final_copy(L, cur, gout);
+  return true;
+}
+
+// Delta::decompress of a small metadata part (thread 0; delta_compressor.cc:
+// 251-273, bytes past the values zeroed as tdbg_general.h); false on anomaly
+__device__ bool delta_serial(const uint8_t* src, uint32_t cn, uint8_t* dst, uint32_t un, uint32_t W) {
+  if (cn < 8) return false;
+  uint64_t num = 0;
+  for (int i = 0; i < 8; i++) num |= (uint64_t)src[i] << (8 * i);
+  const uint64_t nv = num ? num : 1;
+  if (nv > (cn - 8) / W || nv > un / W) return false;
+  const uint64_t m = wmask(W);
+  uint64_t x = 0;
+  for (uint64_t i = 0; i < nv; i++) {
+    uint64_t d = 0;
+    for (uint32_t b = 0; b < W; b++) d |= (uint64_t)src[8 + i * W + b] << (8 * b);
+    x = (x + d) & m;
+    for (uint32_t b = 0; b < W; b++) dst[i * W + b] = (uint8_t)(x >> (8 * b));
+  }
+  for (uint64_t i = nv * W; i < un; i++) dst[i] = 0;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// CompressionFilter + Delta::decompress<T> (compression_filter.cc:303-347,
+// delta_compressor.cc:251-273) for 4- / 8-byte values: the data part
+// [u64 num][T x0][T d1 ..] is an inclusive prefix sum (mod 2^8W).  Fused for
+// one data part whose values fill it exactly (un == num W, num >= 1); each
+// thread sums its slice of values in registers, the block scan carries.
+// ---------------------------------------------------------------------------
+template <int W, bool SWZ>
+__device__ __forceinline__ bool f_delta(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+                                        uint8_t* gout, uint32_t cap) {
+  typedef typename std::conditional<(W == 8), uint64_t, uint32_t>::type U;
+  uint32_t nmd, src, c, u, mdt;
+  if (!comp_header(L, cur, mo, mn, nmd, src, c, u, mdt)) return false;
+  if (c < 8 || (final && u > cap) || u > (uint32_t)(FNT * SP)) return false;
+  const uint64_t num = ldsn(L.X, src, 8);
+  if (num == 0 || num * W != u || 8 + num * W > c) return false;
+  // aligned window reads of every thread stay inside L.X
+  if (src + 8 + (uint32_t)(FNT * SP) + 8 > XCAP) return false;
+  if (tid_() == 0) {
+    bool ok = true;
+    uint32_t o = 0;
+    for (uint32_t i = 0; i < nmd; i++) {
+      const uint32_t un = L.pairs[3 * i], cn = L.pairs[3 * i + 1], ip = L.pairs[3 * i + 2];
+      ok = ok && delta_serial(L.X + cur.base + ip, cn, L.MD + o, un, W);
+      o += un;
+    }
+    L.flag[0] = ok ? 0u : 1u;
+  }
+  __syncthreads();
+  if (L.flag[0]) return false;
+  mo = 0;
+  mn = mdt;
+  // thread t: values [t EP, t EP + EP) = bytes [t SP, t SP + SP) of the part
+  constexpr int EP = SP / W;
+  const uint32_t t = tid_();
+  const uint32_t sb = src + 8 + t * SP;
+  const uint32_t a = sb & ~3u, sh = sb & 3u;
+  uint32_t A[SPD + 1];
+#pragma unroll
+  for (int k = 0; k <= SPD; k++) A[k] = *(const uint32_t*)(L.X + a + 4 * k);
+  uint32_t r[SPD];
+#pragma unroll
+  for (int k = 0; k < SPD; k++) r[k] = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sh);
+  U acc = 0;
+#pragma unroll
+  for (int e = 0; e < EP; e++) {
+    acc += (U)rget<W>(r, e);
+    rset<W>(r, e, acc);
+  }
+  const U ex = block_exscan_op<0, U>(acc, (U*)L.red);
+#pragma unroll
+  for (int e = 0; e < EP; e++) rset<W>(r, e, (U)rget<W>(r, e) + ex);
+  __syncthreads();  // every part read before the values overwrite it
+  const uint32_t n = u;
+  const bool swz = SWZ && W == 4 && ((n >> 2) & 3) == 0;
+  {
+    const uint32_t s0 = t * SP, rot = swz ? (t & 7) : 0u;
+#pragma unroll
+    for (int q = 0; q < SP / 16; q++) {
+      const uint32_t o = s0 + 16 * q;
+      if (o < n) *(uint4*)(L.X + s0 + 16 * (q ^ rot)) = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+    }
+  }
+  __syncthreads();
+  cur.base = 0;
+  cur.n = n;
+  cur.swz = swz ? 1u : 0u;
+  if (final) final_copy(L, cur, gout);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// FLOAT_SCALE^-1 (FloatScalingFilter::run_reverse<T, W>,
+// float_scaling_filter.cc:164-197): element-wise T(scale * double(W int) +
+// offset), product and sum rounded separately as tdbg_general.h.  One part;
+// output units of 16 B gathered in registers (in place) or streamed.
+// ---------------------------------------------------------------------------
+template <int BW, int TS>
+__device__ __forceinline__ uint32_t fscale_one(int64_t q, double sc, double of, uint32_t& hi) {
+  if (TS == 4) {
+    const float e = __ll2float_rn(q);
+    double prod = sc * (double)e;
+    asm volatile("" : "+v"(prod));  // keeps the product rounded: no v_fma_f64
+    hi = 0;
+    return __float_as_uint(__double2float_rn(prod + of));
+  } else {
+    double prod = sc * __ll2double_rn(q);
+    asm volatile("" : "+v"(prod));
+    const uint64_t y = (uint64_t)__double_as_longlong(prod + of);
+    hi = (uint32_t)(y >> 32);
+    return (uint32_t)y;
+  }
+}
+
+template <int BW, int TS>
+__device__ __forceinline__ bool f_fscale(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn, bool final,
+                                         uint8_t* gout, uint32_t cap, double sc, double of) {
+  if (mn < 8) return false;
+  const uint32_t np = lds32(L.MD, mo), ps = lds32(L.MD, mo + 4);
+  if (np != 1 || ps > cur.n) return false;
+  const uint32_t ne = ps / BW, on = ne * TS;
+  if (final ? on > cap : on > XCAP) return false;
+  mo += 8;
+  mn -= 8;
+  const uint8_t* X = L.X;
+  const uint32_t base = cur.base;
+  constexpr int EPU = 16 / TS;  // values per 16-B output unit
+  auto elem = [&](uint32_t j) -> int64_t {
+    return sext64(ldsn(X, base + j * BW, BW), BW);
+  };
+  auto unit = [&](uint32_t u, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int k = 0; k < EPU; k++) {
+      uint32_t hi;
+      const uint32_t lo = fscale_one<BW, TS>(elem(EPU * u + k), sc, of, hi);
+      if (TS == 4) w[k] = lo;
+      else { w[2 * k] = lo; w[2 * k + 1] = hi; }
+    }
+  };
+  auto part = [&](uint32_t u, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = 0;
+#pragma unroll
+    for (int k = 0; k < EPU; k++) {
+      const uint32_t j = EPU * u + k;
+      if (j < ne) {
+        uint32_t hi;
+        const uint32_t lo = fscale_one<BW, TS>(elem(j), sc, of, hi);
+        if (TS == 4) w[k] = lo;
+        else { w[2 * k] = lo; w[2 * k + 1] = hi; }
+      }
+    }
+  };
+  drive2<16>(L, on, on / 16, final, gout, unit, part);
+  cur.base = 0;
+  cur.n = on;
+  cur.swz = 0;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // compile-time pipeline specs
 // ---------------------------------------------------------------------------
 // Stage code: kind | W << 4 | signed << 8 (0 = no stage).  A spec lists the
@@ -1639,8 +1891,13 @@ __device__ __forceinline__ bool f_rle(FastLds& L, View& cur, uint32_t& mo, uint3
 template <int CODE, int POS, int NEXT, class M>
 __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, uint32_t& mn,
                                           bool final, uint8_t* gout, uint32_t cap,
-                                          const tdbg_stage& s, M&& mark) {
+                                          const tdbg_plan& P, M&& mark) {
+  const tdbg_stage& s = P.s[POS];
   constexpr int K = CODE & 15, W = (CODE >> 4) & 15, SG = (CODE >> 8) & 1;
+  // the next stage reads a swizzled view: slice stages (PD, XOR), or a
+  // 4-byte byteshuffle (whole plane units)
+  constexpr bool NEXT_SLICE = (NEXT & 15) == TDBG_K_PD || (NEXT & 15) == TDBG_K_XOR;
+  constexpr bool NEXT_B4 = NEXT == SC(TDBG_K_BYTESHUFFLE, 4, 0);
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (K == TDBG_K_PASS) {
     if (final) {
@@ -1653,15 +1910,23 @@ __device__ __forceinline__ bool run_stage(FastLds& L, View& cur, uint32_t& mo, u
   } else if constexpr (K == TDBG_K_BITSHUFFLE) {
     return f_bitshuffle<W>(L, cur, mo, mn, final, gout, cap);
   } else if constexpr (K == TDBG_K_BWR) {
-    return f_bwr<W, SG != 0>(L, cur, mo, mn, final, gout, cap, s.dts, POS, mark);
+    return f_bwr<W, SG != 0, NEXT_SLICE ? 1 : NEXT_B4 ? 2 : 0>(L, cur, mo, mn, final, gout, cap, s.dts, POS, mark);
   } else if constexpr (K == TDBG_K_PD) {
-    return f_pd<W>(L, cur, mo, mn, final, gout, cap, s.dts);
+    return f_pd<W, NEXT_SLICE ? 1 : NEXT_B4 ? 2 : 0>(L, cur, mo, mn, final, gout, cap, s.dts);
   } else if constexpr (K == TDBG_K_DD) {
     // the next stage (the one run after this) is a 4-byte byteshuffle
     constexpr bool SWZ = NEXT == SC(TDBG_K_BYTESHUFFLE, 4, 0);
     return f_dd<W, SWZ>(L, cur, mo, mn, final, gout, cap, mark);
   } else if constexpr (K == TDBG_K_RLE) {
     return f_rle(L, cur, mo, mn, final, gout, cap, (uint32_t)s.cs);
+  } else if constexpr (K == TDBG_K_XOR) {
+    return f_xor<W, NEXT_SLICE ? 1 : NEXT_B4 ? 2 : 0>(L, cur, mo, mn, final, gout, cap);
+  } else if constexpr (K == TDBG_K_DELTA) {
+    constexpr bool SWZ = NEXT == SC(TDBG_K_BYTESHUFFLE, 4, 0);
+    return f_delta<W, SWZ>(L, cur, mo, mn, final, gout, cap);
+  } else if constexpr (K == TDBG_K_FSCALE) {
+    // W = byte width of the stored integers, SG: the float type is 8 bytes
+    return f_fscale<W, SG ? 8 : 4>(L, cur, mo, mn, final, gout, cap, P.fs_scale[POS], P.fs_offset[POS]);
   } else {
     return false;
   }
@@ -1704,25 +1969,25 @@ __device__ __forceinline__ bool f_resident(const tdbg_plan& P, View cur, uint32_
   // reverse order: the last filter runs first (filter_pipeline.cc:470-513)
   if constexpr (S3 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < 1) return true;
-    if (!run_stage<S3, 3, S2>(L, cur, mo, mn, false, gout, orig, P.s[3], mark)) return false;
+    if (!run_stage<S3, 3, S2>(L, cur, mo, mn, false, gout, orig, P, mark)) return false;
     if (cur.n > XCAP) return false;
     mark(2);
   }
   if constexpr (S2 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S2, 2, (S1 != 0 ? S1 : S0)>(L, cur, mo, mn, false, gout, orig, P.s[2], mark)) return false;
+    if (!run_stage<S2, 2, (S1 != 0 ? S1 : S0)>(L, cur, mo, mn, false, gout, orig, P, mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 3 : 2);
   }
   if constexpr (S1 != 0) {
     if (dbg_stop > 1 && dbg_stop - 1 < (S3 != 0 ? 3u : S2 != 0 ? 2u : 1u)) return true;
-    if (!run_stage<S1, 1, S0>(L, cur, mo, mn, false, gout, orig, P.s[1], mark)) return false;
+    if (!run_stage<S1, 1, S0>(L, cur, mo, mn, false, gout, orig, P, mark)) return false;
     if (cur.n > XCAP) return false;
     mark(S3 != 0 ? 4 : S2 != 0 ? 3 : 2);
   }
   if (dbg_stop > 1) return true;
   hook();
-  const bool ok = run_stage<S0, 0, 0>(L, cur, mo, mn, true, gout, orig, P.s[0], mark);
+  const bool ok = run_stage<S0, 0, 0>(L, cur, mo, mn, true, gout, orig, P, mark);
   mark(5);
   return ok;
 }
@@ -1987,6 +2252,9 @@ unfilter_fused_kernel(const KParams kp) {
 #define K_PD TDBG_K_PD
 #define K_DD TDBG_K_DD
 #define K_RLE TDBG_K_RLE
+#define K_XOR TDBG_K_XOR
+#define K_DELTA TDBG_K_DELTA
+#define K_FSCALE TDBG_K_FSCALE
 #define SPECS(X)                                                        \
   /* C1: [BYTESHUFFLE] int32 / int64 / int16 */                          \
   X(1, SC(K_BYTE, 4, 0), 0, 0, 0)                                        \
@@ -2021,7 +2289,18 @@ unfilter_fused_kernel(const KParams kp) {
   X(24, SC(K_DD, 8, 0), SC(K_BWR, 8, 0), 0, 0)                           \
   X(25, SC(K_BWR, 4, 1), 0, 0, 0)                                        \
   X(26, SC(K_BWR, 8, 0), 0, 0, 0)                                        \
-  X(27, SC(K_BWR, 8, 1), 0, 0, 0)
+  X(27, SC(K_BWR, 8, 1), 0, 0, 0)                                        \
+  /* XOR / DELTA / FLOAT_SCALE pipelines */                              \
+  X(28, SC(K_XOR, 4, 0), SC(K_BWR, 4, 1), 0, 0)                          \
+  X(29, SC(K_XOR, 8, 0), SC(K_BWR, 8, 1), 0, 0)                          \
+  X(30, SC(K_XOR, 4, 0), 0, 0, 0)                                        \
+  X(31, SC(K_XOR, 8, 0), 0, 0, 0)                                        \
+  X(32, SC(K_BYTE, 4, 0), SC(K_DELTA, 4, 0), SC(K_BWR, 4, 1), 0)         \
+  X(33, SC(K_DELTA, 4, 0), 0, 0, 0)                                      \
+  X(34, SC(K_DELTA, 8, 0), 0, 0, 0)                                      \
+  X(35, SC(K_FSCALE, 4, 1), SC(K_BWR, 4, 1), 0, 0)                       \
+  X(36, SC(K_FSCALE, 4, 0), 0, 0, 0)                                     \
+  X(37, SC(K_FSCALE, 8, 1), SC(K_BWR, 8, 1), 0, 0)
 
 // The spec table is compiled as TDBG_NPART translation units (the build
 // passes -DTDBG_PART=k): part k instantiates the kernels whose id % NPART == k,
@@ -2038,7 +2317,10 @@ static uint32_t stage_code(const tdbg_stage& s) {
     case TDBG_K_RLE: return SC(TDBG_K_RLE, 0, 0);
     case TDBG_K_BWR: return SC(TDBG_K_BWR, s.w, s.sgn ? 1 : 0);
     case TDBG_K_PD: case TDBG_K_DD: case TDBG_K_BYTESHUFFLE: case TDBG_K_BITSHUFFLE:
+    case TDBG_K_XOR: case TDBG_K_DELTA:
       return SC(s.kind, s.w, 0);
+    case TDBG_K_FSCALE:  // w = stored byte width, sign field = 8-byte float type
+      return SC(TDBG_K_FSCALE, s.w, s.dts == 8 ? 1 : 0);
     default: return 0xffffffffu;
   }
 }

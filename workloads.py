@@ -324,7 +324,8 @@ def config(name: str):
     """(serialized pipeline, on-disk datatype, cell size, values(variant, k, rng), tile(values))."""
     from tiledb_amd.filter_pipeline import (BitshuffleFilter, BitWidthReductionFilter,
                                             ByteshuffleFilter, CompressionFilter, Compressor,
-                                            Datatype, FilterPipeline, PositiveDeltaFilter)
+                                            Datatype, FilterPipeline, FloatScalingFilter,
+                                            PositiveDeltaFilter, XORFilter)
     dd = CompressionFilter(Compressor.DOUBLE_DELTA, -1)
     rle = CompressionFilter(Compressor.RLE, -1)
     P = lambda *f: FilterPipeline(65536, list(f)).serialize()  # noqa: E731
@@ -339,15 +340,40 @@ def config(name: str):
         "c4": (P(PositiveDeltaFilter(1024), BitWidthReductionFilter(256)), Datatype.UINT64, 8,
                lambda var, k, rng: c4_values(k, rng), c4_tile),
         "c5": (c5_pipeline_bytes(), Datatype.INT32, 4, c5_values, c5_filter_tile),
+        # XOR / DELTA / FLOAT_SCALE pipelines: tiles are
+        # encoded by the device forward path (tile = None; bench.py)
+        "xor": (P(XORFilter(), BitWidthReductionFilter(256)), Datatype.FLOAT32, 4,
+                lambda var, k, rng: c2_values(k, rng), None),
+        "delta": (P(ByteshuffleFilter(), CompressionFilter(Compressor.DELTA, -1), BitWidthReductionFilter(256)),
+                  Datatype.INT32, 4, c5_values, None),
+        "fscale": (P(FloatScalingFilter(1e-3, 0.0, 4), BitWidthReductionFilter(256)), Datatype.FLOAT64, 8,
+                   lambda var, k, rng: np.sin(1e-2 * np.arange(8192) + k) + rng.normal(0, 1e-4, 8192), None),
     }
     return table[name]
 
 
-def pool(name: str, variant: str, nunique: int, seed: int):
-    """nunique distinct on-disk tiles of a config + their unfiltered values."""
+def expected(name: str, v: np.ndarray) -> np.ndarray:
+    """The values an unfilter of the config's tiles returns: the input, except
+    FLOAT_SCALE's lossy quantization (float_scaling_filter.cc:60-99, 164-197:
+    q = round((x - offset) / scale) to the stored width, then
+    scale * double(q) + offset, each operation rounded once)."""
+    if name != "fscale":
+        return v
+    q = (v - 0.0) / 1e-3
+    q = (np.sign(q) * np.floor(np.abs(q) + 0.5)).astype(np.int64).astype(np.int32)  # std::round
+    return 1e-3 * q.astype(np.float64) + 0.0
+
+
+def pool(name: str, variant: str, nunique: int, seed: int, encode=None):
+    """nunique distinct on-disk tiles of a config + their unfiltered values.
+    Configs without a numpy encoder take `encode(values list) -> tiles`."""
     ser, dt, cs, values, tile = config(name)
     rng = np.random.default_rng(seed)
     vals = [values(variant, k, rng) for k in range(nunique)]
+    if tile is None:
+        if encode is None:
+            raise ValueError(f"{name}: tiles are encoded by the device forward path")
+        return encode(vals), vals
     return [tile(v) for v in vals], vals
 
 
