@@ -115,6 +115,13 @@ enum tdbg_status {
 
 /* unfilter flags */
 #define TDBG_TILE_OFFSETS 0x1u /* offsets tile: expected size = out_size - 8 (tile.cc:241-248) */
+/* Chunk-parallel launch: a device pass first builds the chunk directory of
+ * every tile (Tile::load_chunk_data, tile.cc:280-313) and the fused kernel
+ * then takes chunks, not tiles, as work items -- the tile x chunk-range split
+ * of reader_base.cc:970-989 on the device, for batches of few, multi-chunk
+ * tiles.  Results and statuses are those of a tile launch.  Applied
+ * automatically when a launch has fewer tiles than the device has CUs. */
+#define TDBG_CHUNK_PARALLEL 0x8u
 /* tdbg_unfilter_tiles_host only: every input tile of the call lies in ONE host
  * allocation (e.g. a FilteredData block, filtered_data.h:152-644), so tiles
  * separated by at most 64 B of padding may move in one H2D copy (padding
@@ -200,6 +207,26 @@ int tdbg_unfilter_tiles_host(tdbg_context* ctx, const tdbg_pipeline* p,
                              const uint64_t* filtered_size, uint8_t* const* out,
                              const uint64_t* out_size, uint32_t flags,
                              int32_t* host_status, uint64_t batch_bytes);
+
+/* Tile::add_extra_offset (tile.h:144-146, called after an offsets tile is
+ * unfiltered at reader_base.cc:893): for every tile whose d_status entry is
+ * TDBG_OK (every tile when d_status is NULL), the last 8 bytes of d_out[i]
+ * (the extra slot a TDBG_TILE_OFFSETS unfilter leaves) become d_var_size[i],
+ * the size of the tile's var-data tile.  Device arrays; enqueued on stream. */
+int tdbg_add_extra_offsets_async(tdbg_context* ctx, uint64_t ntiles, uint8_t* const* d_out,
+                                 const uint64_t* d_out_size, const uint64_t* d_var_size,
+                                 const int32_t* d_status, tdbg_stream stream);
+
+/* tdbg_unfilter_tiles_host for offsets tiles with the extra offset fused
+ * before the D2H: flags must include TDBG_TILE_OFFSETS; var_size (host array,
+ * one per tile) is copied with the batch's pointer arrays and written into
+ * each tile's last 8 bytes on the device, so the result buffers receive
+ * complete offsets tiles in the same copy (reader_base.cc:885-893). */
+int tdbg_unfilter_offsets_host(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t ntiles,
+                               const uint8_t* const* filtered, const uint64_t* filtered_size,
+                               uint8_t* const* out, const uint64_t* out_size,
+                               const uint64_t* var_size, uint32_t flags, int32_t* host_status,
+                               uint64_t batch_bytes);
 
 /* Contiguous tile shards balanced by filtered + unfiltered bytes: shard k is
  * tiles [cuts[k], cuts[k+1]), cuts has nshards + 1 entries.  Host-only; the

@@ -379,3 +379,139 @@ def test_filter_pipeline_run_reverse_api(eng, oracle_mod):
     assert np.array_equal(batch.output(0), t)
     with pytest.raises(FilterStatusException):
         case.pipeline.run_reverse([f[:100]], [osz], case.dtype, case.cell_size)
+
+
+def _offsets_cases():
+    return [c for c in config_cases(2) + edge_cases() if c.offsets_tile]
+
+
+def test_add_extra_offset_device(eng, ctx, oracle_mod):
+    """Tile::add_extra_offset (tile.h:144-146) after a TDBG_TILE_OFFSETS
+    unfilter: the tile's values, then its var tile's size in the last u64;
+    an errored tile is left alone."""
+    rng = np.random.default_rng(7)
+    cases = _offsets_cases()
+    assert cases
+    for case in cases:
+        op, enc = encode(oracle_mod, case)
+        if not enc:
+            continue
+        filt = [e[0] for e in enc]
+        osz = [e[2] for e in enc]
+        # one corrupted copy: its status is an error, its slot keeps the fill
+        bad = filt[0].copy()
+        bad[:8] = 0xff
+        filt2, osz2 = filt + [bad], osz + [osz[0]]
+        dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+        batch = eng.TileBatch.from_host(filt2, osz2, fill=0x5a)
+        var = rng.integers(0, 2**40, len(filt2)).astype(np.uint64)
+        ctx.unfilter_async(dp, batch, offsets_tiles=True)
+        ctx.add_extra_offsets(batch, var)
+        st = batch.d_status[: batch.ntiles].cpu().numpy()
+        for i, f in enumerate(filt2):
+            rc, ref = op.unfilter_tile(f, osz2[i], True, fill=0x5a)
+            assert int(st[i]) == rc
+            got = batch.output(i)
+            if rc:
+                assert np.all(got[-8:] == 0x5a), "an errored tile's extra slot was written"
+                continue
+            assert np.array_equal(got[:-8], ref[:-8])
+            assert int(got[-8:].view(np.uint64)[0]) == int(var[i])
+
+
+def test_add_extra_offset_host_fused(eng, ctx, oracle_mod):
+    """tdbg_unfilter_offsets_host: the extra offset is written on the device
+    before the D2H, so the host result holds the complete offsets tile."""
+    rng = np.random.default_rng(8)
+    for case in _offsets_cases():
+        op, enc = encode(oracle_mod, case)
+        if not enc:
+            continue
+        filt = [e[0] for e in enc] * 3
+        osz = np.array([e[2] for e in enc] * 3, dtype=np.uint64)
+        var = rng.integers(0, 2**40, len(filt)).astype(np.uint64)
+        sizes = np.array([f.size for f in filt], dtype=np.uint64)
+        offs = eng.pack_offsets(sizes, 1)
+        packed = np.zeros(int(offs[-1] + sizes[-1]), dtype=np.uint8)
+        for f, o in zip(filt, offs):
+            packed[int(o):int(o) + f.size] = f
+        out = np.zeros(int(osz.sum()), dtype=np.uint8)
+        oo = np.zeros_like(osz)
+        oo[1:] = np.cumsum(osz)[:-1]
+        st = ctx.unfilter_host(dp := eng.DevicePipeline(case.serialized, case.version, int(case.dtype),
+                                                        case.cell_size),
+                               offs + np.uint64(packed.ctypes.data), sizes, oo + np.uint64(out.ctypes.data), osz,
+                               var_size=var, batch_bytes=1 << 20, contiguous_input=True,
+                               contiguous_output=True)
+        assert not st.any()
+        for i, f in enumerate(filt):
+            rc, ref = op.unfilter_tile(f, int(osz[i]), True)
+            assert rc == 0
+            got = out[int(oo[i]):int(oo[i] + osz[i])]
+            assert np.array_equal(got[:-8], ref[:-8])
+            assert int(got[-8:].view(np.uint64)[0]) == int(var[i])
+        del dp
+
+
+@pytest.mark.parametrize("ntiles,nvalues,max_chunk,flag", [
+    (4, 262144, 0, False),        # 4 x 1 MiB tiles, 16 chunks each: fewer tiles than CUs (auto)
+    (300, 16384, 8192, True),     # 300 x 64 KiB tiles, 8 chunks each: TDBG_CHUNK_PARALLEL
+])
+def test_chunk_parallel_multichunk(eng, ctx, oracle_mod, ntiles, nvalues, max_chunk, flag):
+    """Chunk-parallel launches (device chunk directory, tdbg_chunkdir.hip):
+    bit-exact with the oracle, every tile taken by the fused kernel."""
+    import workloads as W
+    from tiledb_amd.filter_pipeline import Datatype
+    ser = W.c5_pipeline_bytes()
+    op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.INT32), 4)
+    dp = eng.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+    rng = np.random.default_rng(11)
+    vals = [np.concatenate([W.c5_values("active", k, rng) for _ in range(nvalues // 16384)])
+            for k in range(min(ntiles, 8))]
+    enc = [np.frombuffer(op.filter_tile(v.view(np.uint8), None, max_chunk), dtype=np.uint8) for v in vals]
+    filt = [enc[i % len(enc)] for i in range(ntiles)]
+    osz = [vals[i % len(vals)].nbytes for i in range(ntiles)]
+    batch = eng.TileBatch.from_host(filt, osz)
+    f0, b0, _ = ctx.path_stats()
+    st = ctx.unfilter(dp, batch, chunk_parallel=flag)
+    f1, b1, _ = ctx.path_stats()
+    assert not st.any()
+    assert b1 - b0 == 0 and f1 - f0 == ntiles
+    out = batch.outputs_host()
+    for i in range(ntiles):
+        o = int(batch.out_off[i])
+        assert np.array_equal(out[o:o + osz[i]], vals[i % len(vals)].view(np.uint8)), f"tile {i}"
+
+
+def test_chunk_parallel_corrupt_mix(eng, ctx, oracle_mod):
+    """Chunk mode with corrupted tiles among good ones: statuses as the
+    oracle's (header errors from the directory pass, chunk errors through the
+    general interpreter), good tiles bit-exact."""
+    import workloads as W
+    from tiledb_amd.filter_pipeline import Datatype
+    ser = W.c5_pipeline_bytes()
+    op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.INT32), 4)
+    dp = eng.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+    rng = np.random.default_rng(12)
+    v = np.concatenate([W.c5_values("active", k, rng) for k in range(4)])
+    good = np.frombuffer(op.filter_tile(v.view(np.uint8), None, 0), dtype=np.uint8)
+    tiles = []
+    for k in range(24):
+        t = good.copy()
+        if k % 4 == 1:
+            t[:8] = 0x7f                      # chunk count: header walk fails
+        elif k % 4 == 2:
+            t[8 + 12 + 4 * (k % 5)] ^= 0x5a   # chunk metadata byte
+        elif k % 4 == 3:
+            t[len(t) // 2] ^= 0xff            # data byte
+        tiles.append(t)
+    osz = [v.nbytes] * len(tiles)
+    batch = eng.TileBatch.from_host(tiles, osz)
+    st = ctx.unfilter(dp, batch, chunk_parallel=True)
+    out = batch.outputs_host()
+    for i, t in enumerate(tiles):
+        rc, ref = op.unfilter_tile(t, osz[i])
+        assert int(st[i]) == rc, f"tile {i}: gpu {st[i]} oracle {rc}"
+        if rc == 0:
+            o = int(batch.out_off[i])
+            assert np.array_equal(out[o:o + osz[i]], ref)

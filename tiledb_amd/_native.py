@@ -46,6 +46,9 @@ SIGNATURES = {
                                                 ctypes.c_uint32, c_i32p, c_vp]),
     "tdbg_unfilter_tiles_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
                                                 ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
+    "tdbg_unfilter_offsets_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                  ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
+    "tdbg_add_extra_offsets_async": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "tdbg_unfilter_tiles_multi_gpu": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
                                                      ctypes.c_uint32, c_i32p,
                                                      ctypes.POINTER(ctypes.c_int), ctypes.c_int,

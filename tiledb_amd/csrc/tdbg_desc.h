@@ -65,6 +65,16 @@ const tdbg_plan* tdbg_internal_plan(const tdbg_pipeline* p);  // null if unsuppo
 void tdbg_internal_set_error(const char* msg);                // tdbg_last_error text
 
 namespace tdbg {
+// One chunk of the device chunk directory (Tile::load_chunk_data,
+// tile.cc:280-313, built on the device for every tile of a launch)
+struct ChunkRec {
+  uint32_t tile;      // index into the launch's tile arrays
+  uint32_t ml, fl;    // chunk metadata / filtered data bytes
+  uint32_t orig;      // unfiltered bytes
+  uint64_t in_off;    // byte offset of the chunk's metadata in the filtered tile
+  uint64_t out_off;   // byte offset of the chunk's output in the tile
+};
+
 // kernel parameters (passed by value)
 struct KParams {
   const uint8_t* const* in;
@@ -97,6 +107,10 @@ struct KParams {
   uint64_t* out_len;
   uint64_t cell_size;
   uint32_t max_chunk;
+  // chunk-parallel launches: the device chunk directory (chunks[k], k <
+  // *nchunks) replaces the tile loop of the fused kernel
+  const ChunkRec* chunks;
+  const uint32_t* nchunks;
   tdbg_plan plan;
 };
 

@@ -2115,6 +2115,45 @@ unfilter_fused_kernel(const KParams kp) {
   pf.cnt = 0;
   pf.base = 0;
   constexpr bool PF = pf_enabled(S0, S1, S2, S3);
+  if (kp.chunks) {
+    // chunk-parallel launch (TDBG_CHUNK_PARALLEL): work items are the
+    // records of the device chunk directory (tdbg_chunkdir.hip); a chunk the
+    // fused path declines sends its whole tile to the general interpreter
+    // (first decline wins the status, queues the tile, and takes it out of
+    // the fused counters the directory pass added it to)
+    const uint32_t nck = __builtin_amdgcn_readfirstlane(*kp.nchunks);
+    for (uint32_t j = blockIdx.x; j < nck; j += (uint32_t)G) {
+      const ChunkRec* rp = kp.chunks + j;
+      const uint32_t tile = __builtin_amdgcn_readfirstlane(rp->tile);
+      const uint32_t ml = __builtin_amdgcn_readfirstlane(rp->ml);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(rp->fl);
+      const uint32_t orig = __builtin_amdgcn_readfirstlane(rp->orig);
+      const uint64_t in_off = uni64(rp->in_off), out_off = uni64(rp->out_off);
+      const int32_t st0 = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)kp.status[tile]);
+      bool ok = true;
+      if (st0 == TDBG_OK) {
+        const uint8_t* in = (const uint8_t*)uni64((uint64_t)kp.in[tile]) + in_off;
+        uint8_t* out = (uint8_t*)uni64((uint64_t)kp.out[tile]) + out_off;
+        ok = f_chunk<S0, S1, S2, S3>(kp.plan, in, ml, in + ml, fl, out, orig, L, kp.dbg_stop);
+      }
+      __syncthreads();  // LDS reads of this chunk done before the next load
+      if (!ok && tid_() == 0) {
+        if (atomicCAS(&kp.status[tile], (int32_t)TDBG_OK, (int32_t)TDBG_E_FALLBACK) == TDBG_OK) {
+          if (kp.fbq) {
+            const uint32_t k = atomicAdd(kp.fbq, 1u);
+            if (k < kp.fbq_cap) kp.fbq[1 + k] = tile;
+          }
+          if (kp.stats) {
+            atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], ~0ull);
+            atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES],
+                      (unsigned long long)(0 - kp.out_size[tile]));
+          }
+        }
+      }
+    }
+    pc.flush();
+    return;
+  }
   // tiles: all ntiles, or a host-given list (the sync entry's retry)
   const uint64_t ntl = kp.ntiles;
   const uint32_t* tl = kp.tile_list;

@@ -28,6 +28,12 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
 extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
+extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
+                                            tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
+                                            hipStream_t stream);
+extern "C" hipError_t tdbg_launch_extra_offset(uint64_t ntiles, uint8_t* const* out, const uint64_t* out_size,
+                                               const uint64_t* var_size, const int32_t* status,
+                                               hipStream_t stream);
 #define TDBG_NPART_HOST 6  // = TDBG_NPART of the build (tiledb_amd/build.py)
 #define TDBG_DECL_PART(k) \
   extern "C" hipError_t tdbg_launch_fast_part##k(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
@@ -129,6 +135,13 @@ struct tdbg_context {
   // forward (filter) scratch slots
   uint8_t* fscratch = nullptr;
   uint64_t fscratch_bytes = 0;
+  // device chunk directory (chunk-parallel launches): per-tile counts and
+  // record bases, the records, the placed-record count
+  uint32_t* dir_cnt = nullptr;
+  uint32_t* dir_base = nullptr;
+  tdbg::ChunkRec* dir_recs = nullptr;
+  uint32_t* dir_total = nullptr;
+  uint64_t dir_tiles = 0, dir_cap = 0;
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -509,6 +522,10 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->rscratch) (void)hipFree(c->rscratch);
   if (c->fscratch) (void)hipFree(c->fscratch);
+  if (c->dir_cnt) (void)hipFree(c->dir_cnt);
+  if (c->dir_base) (void)hipFree(c->dir_base);
+  if (c->dir_recs) (void)hipFree(c->dir_recs);
+  if (c->dir_total) (void)hipFree(c->dir_total);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -590,6 +607,40 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   }
   // the queue starts empty for this launch, whatever ran before on any stream
   if (queued) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
+  // Chunk-parallel: asked for, or fewer tiles than CUs (tiles, not chunks,
+  // would then bound the parallelism).  The directory pass runs first on
+  // the same stream; its records feed the fused kernel.
+  const bool chunked = queued && !d_list && ((flags & TDBG_CHUNK_PARALLEL) || ntiles < (uint64_t)c->cus);
+  if (chunked) {
+    const uint64_t want = std::max<uint64_t>(4 * ntiles, 4096);
+    if (ntiles > c->dir_tiles || want > c->dir_cap) {
+      HIP_OK(hipStreamSynchronize(stream));  // earlier launches may still read the old directory
+      if (ntiles > c->dir_tiles) {
+        if (c->dir_cnt) HIP_OK(hipFree(c->dir_cnt));
+        if (c->dir_base) HIP_OK(hipFree(c->dir_base));
+        c->dir_cnt = nullptr;
+        c->dir_base = nullptr;
+        c->dir_tiles = 0;
+        HIP_OK(hipMalloc(&c->dir_cnt, ntiles * 4));
+        HIP_OK(hipMalloc(&c->dir_base, ntiles * 4));
+        c->dir_tiles = ntiles;
+      }
+      if (want > c->dir_cap) {
+        if (c->dir_recs) HIP_OK(hipFree(c->dir_recs));
+        c->dir_recs = nullptr;
+        c->dir_cap = 0;
+        HIP_OK(hipMalloc(&c->dir_recs, want * sizeof(tdbg::ChunkRec)));
+        c->dir_cap = want;
+      }
+    }
+    if (!c->dir_total) HIP_OK(hipMalloc(&c->dir_total, 4));
+    hipError_t e = tdbg_launch_chunk_dir(&kp, c->dir_cnt, c->dir_base, c->dir_recs,
+                                         (uint32_t)std::min<uint64_t>(c->dir_cap, 0xffffffffull), c->dir_total,
+                                         stream);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("chunk directory launch: ") + hipGetErrorString(e));
+    kp.chunks = c->dir_recs;
+    kp.nchunks = c->dir_total;
+  }
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   // Events only on armed launches (tdbg_context_time_launches): an event
   // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
@@ -983,8 +1034,8 @@ static int stage_reserve(tdbg_context::Stage& s, uint64_t in_b, uint64_t out_b, 
     if (s.h_status) HIP_OK(hipHostFree(s.h_status));
     if (s.d_stat) HIP_OK(hipFree(s.d_stat));
     HIP_OK(hipMalloc(&s.d_stat, nt * 4));
-    HIP_OK(hipMalloc(&s.d_ptrs, nt * 32));
-    HIP_OK(hipHostMalloc((void**)&s.h_ptrs, nt * 32));
+    HIP_OK(hipMalloc(&s.d_ptrs, nt * 40));
+    HIP_OK(hipHostMalloc((void**)&s.h_ptrs, nt * 40));
     HIP_OK(hipHostMalloc((void**)&s.h_status, nt * 4));
     s.ptr_cap = nt;
   }
@@ -1042,10 +1093,10 @@ static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* 
   return TDBG_OK;
 }
 
-int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
-                             const uint8_t* const* in, const uint64_t* in_size,
-                             uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
-                             int32_t* host_status, uint64_t batch_bytes) {
+static int unfilter_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                         const uint8_t* const* in, const uint64_t* in_size,
+                         uint8_t* const* out, const uint64_t* out_size, const uint64_t* var_size,
+                         uint32_t flags, int32_t* host_status, uint64_t batch_bytes) {
   if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
   if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
   if (ntiles == 0) return TDBG_OK;
@@ -1112,7 +1163,9 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
       hos[i - lo] = out_size[i];
       oo += out_size[i];
     }
-    HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, c->hstream));
+    uint64_t* hv = (uint64_t*)(hos + nt);
+    if (var_size) memcpy(hv, var_size + lo, nt * 8);
+    HIP_OK(hipMemcpyAsync(S.d_ptrs, hp, nt * (var_size ? 40 : 32), hipMemcpyHostToDevice, c->hstream));
     rc = copy_ranges(c->hstream, lo, hi, in, in_size, S.d_in, true, nullptr, cin);
     if (rc) return rc;
     const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
@@ -1126,6 +1179,10 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     if (rc) return rc;
     rc = launch(c, p, nt, dp, ds, dop, dos, flags, S.d_stat, c->d_need, nullptr, c->cstream, false);
     if (rc) return rc;
+    if (var_size) {  // Tile::add_extra_offset on the device, before the D2H
+      hipError_t e = tdbg_launch_extra_offset(nt, dop, dos, dos + nt, S.d_stat, c->cstream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("extra offset launch: ") + hipGetErrorString(e));
+    }
     HIP_OK(hipEventRecord(S.kdone, c->cstream));
     HIP_OK(hipStreamWaitEvent(c->dstream, S.kdone, 0));
     HIP_OK(hipMemcpyAsync(S.h_status, S.d_stat, nt * 4, hipMemcpyDeviceToHost, c->dstream));
@@ -1154,6 +1211,7 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
                                   (const uint64_t*)(dp + 3), flags, &one, S.stream);
     st[i] = one;
     if (one == TDBG_OK) HIP_OK(hipMemcpy(out[i], S.d_out, out_size[i], hipMemcpyDeviceToHost));
+    if (one == TDBG_OK && var_size && out_size[i] >= 8) memcpy(out[i] + out_size[i] - 8, &var_size[i], 8);
   }
   if (host_status) memcpy(host_status, st.data(), ntiles * 4);
   for (uint64_t i = 0; i < ntiles; i++)
@@ -1162,6 +1220,36 @@ int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
       snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
       return fail(st[i], msg);
     }
+  return TDBG_OK;
+}
+
+int tdbg_unfilter_tiles_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                             const uint8_t* const* in, const uint64_t* in_size,
+                             uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
+                             int32_t* host_status, uint64_t batch_bytes) {
+  return unfilter_host(c, p, ntiles, in, in_size, out, out_size, nullptr, flags, host_status, batch_bytes);
+}
+
+int tdbg_unfilter_offsets_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
+                               const uint8_t* const* in, const uint64_t* in_size,
+                               uint8_t* const* out, const uint64_t* out_size, const uint64_t* var_size,
+                               uint32_t flags, int32_t* host_status, uint64_t batch_bytes) {
+  if (!(flags & TDBG_TILE_OFFSETS)) return fail(TDBG_E_ARG, "offsets entry without TDBG_TILE_OFFSETS");
+  if (ntiles && !var_size) return fail(TDBG_E_ARG, "null var_size array");
+  return unfilter_host(c, p, ntiles, in, in_size, out, out_size, var_size, flags, host_status, batch_bytes);
+}
+
+int tdbg_add_extra_offsets_async(tdbg_context* c, uint64_t ntiles, uint8_t* const* d_out,
+                                 const uint64_t* d_out_size, const uint64_t* d_var_size,
+                                 const int32_t* d_status, tdbg_stream stream) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (ntiles == 0) return TDBG_OK;
+  if (!d_out || !d_out_size || !d_var_size) return fail(TDBG_E_ARG, "null tile arrays");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  hipError_t e = tdbg_launch_extra_offset(ntiles, d_out, d_out_size, d_var_size, d_status, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("extra offset launch: ") + hipGetErrorString(e));
   return TDBG_OK;
 }
 

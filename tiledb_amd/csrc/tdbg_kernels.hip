@@ -98,3 +98,35 @@ extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
   hipLaunchKernelGGL(tdbg::unfilter_fixup_kernel, dim3(grid), dim3(GEN_NT), 0, stream, *kp);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Tile::add_extra_offset (tile.h:144-146) for unfiltered offsets tiles: the
+// last u64 of the tile (the slot TDBG_TILE_OFFSETS reserves) becomes the size
+// of its var-data tile.  One thread per tile; tiles whose status is an error
+// are left alone.
+// ---------------------------------------------------------------------------
+__global__ void extra_offset_kernel(uint64_t ntiles, uint8_t* const* out, const uint64_t* out_size,
+                                    const uint64_t* var_size, const int32_t* status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  if (status && status[t] != TDBG_OK) return;
+  const uint64_t os = out_size[t];
+  if (os < 8) return;
+  uint8_t* p = out[t] + os - 8;
+  const uint64_t v = var_size[t];
+  if ((((uintptr_t)p) & 7) == 0) {
+    *(uint64_t*)p = v;
+  } else {
+    for (int b = 0; b < 8; b++) p[b] = (uint8_t)(v >> (8 * b));
+  }
+}
+
+extern "C" hipError_t tdbg_launch_extra_offset(uint64_t ntiles, uint8_t* const* out, const uint64_t* out_size,
+                                               const uint64_t* var_size, const int32_t* status,
+                                               hipStream_t stream) {
+  if (ntiles == 0) return hipSuccess;
+  const uint32_t grid = (uint32_t)((ntiles + 255) / 256);
+  hipLaunchKernelGGL(extra_offset_kernel, dim3(grid), dim3(256), 0, stream, ntiles, out, out_size, var_size,
+                     status);
+  return hipGetLastError();
+}

@@ -17,6 +17,7 @@ from ._native import lib
 TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
 HOST_CONTIGUOUS_INPUT = 0x2   # TDBG_HOST_CONTIGUOUS_INPUT
 HOST_CONTIGUOUS_OUTPUT = 0x4  # TDBG_HOST_CONTIGUOUS_OUTPUT
+CHUNK_PARALLEL = 0x8  # TDBG_CHUNK_PARALLEL
 
 
 class EngineError(RuntimeError):
@@ -223,25 +224,25 @@ class Context:
         return int(torch.cuda.current_stream().cuda_stream)
 
     def unfilter(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
-                 stream=None) -> np.ndarray:
+                 stream=None, chunk_parallel: bool = False) -> np.ndarray:
         """Synchronous unfilter; returns the per-tile status array."""
         st = np.zeros(max(batch.ntiles, 1), dtype=np.int32)
         pin, psz, pout, posz = batch.ptrs()
         rc = lib.tdbg_unfilter_tiles_sync(
             self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
-            TILE_OFFSETS if offsets_tiles else 0,
+            (TILE_OFFSETS if offsets_tiles else 0) | (CHUNK_PARALLEL if chunk_parallel else 0),
             st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self._stream(stream))
         if rc and not st[: batch.ntiles].any():
             _check(rc, "tdbg_unfilter_tiles_sync")
         return st[: batch.ntiles]
 
     def unfilter_async(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
-                       stream=None) -> None:
+                       stream=None, chunk_parallel: bool = False) -> None:
         pin, psz, pout, posz = batch.ptrs()
         _check(lib.tdbg_unfilter_tiles_async(
             self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
-            TILE_OFFSETS if offsets_tiles else 0, batch.d_status.data_ptr(),
-            self._stream(stream)), "tdbg_unfilter_tiles_async")
+            (TILE_OFFSETS if offsets_tiles else 0) | (CHUNK_PARALLEL if chunk_parallel else 0),
+            batch.d_status.data_ptr(), self._stream(stream)), "tdbg_unfilter_tiles_async")
 
     def filter_batch(self, dp: DevicePipeline, tiles: Sequence, max_chunk: int = 0) -> "FilterBatch":
         """Device-resident forward batch: the unfiltered tiles packed back to
@@ -313,23 +314,41 @@ class Context:
     def unfilter_host(self, dp: DevicePipeline, in_ptrs: np.ndarray, in_size: np.ndarray,
                       out_ptrs: np.ndarray, out_size: np.ndarray, offsets_tiles: bool = False,
                       batch_bytes: int = 0, contiguous_input: bool = False,
-                      contiguous_output: bool = False) -> np.ndarray:
+                      contiguous_output: bool = False, var_size=None) -> np.ndarray:
         """Host-resident end-to-end (pinned H2D, unfilter, D2H).  contiguous_*:
         the caller states that all input (output) buffers lie in one host
-        allocation, which lets adjacent tiles share one copy."""
+        allocation, which lets adjacent tiles share one copy.  var_size (offsets
+        tiles only): Tile::add_extra_offset fused before the D2H."""
         n = int(in_size.size)
         st = np.zeros(max(n, 1), dtype=np.int32)
         ip = np.ascontiguousarray(in_ptrs, dtype=np.uint64)
         isz = np.ascontiguousarray(in_size, dtype=np.uint64)
         op = np.ascontiguousarray(out_ptrs, dtype=np.uint64)
         osz = np.ascontiguousarray(out_size, dtype=np.uint64)
-        rc = lib.tdbg_unfilter_tiles_host(
-            self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data, op.ctypes.data, osz.ctypes.data,
-            _host_flags(offsets_tiles, contiguous_input, contiguous_output),
-            st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), batch_bytes)
+        flags = _host_flags(offsets_tiles or var_size is not None, contiguous_input, contiguous_output)
+        sp = st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        if var_size is not None:
+            vs = np.ascontiguousarray(var_size, dtype=np.uint64)
+            rc = lib.tdbg_unfilter_offsets_host(self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data,
+                                                op.ctypes.data, osz.ctypes.data, vs.ctypes.data, flags, sp,
+                                                batch_bytes)
+        else:
+            rc = lib.tdbg_unfilter_tiles_host(self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data,
+                                              op.ctypes.data, osz.ctypes.data, flags, sp, batch_bytes)
         if rc and not st[:n].any():
-            _check(rc, "tdbg_unfilter_tiles_host")
+            _check(rc, "tdbg_unfilter_offsets_host" if var_size is not None else "tdbg_unfilter_tiles_host")
         return st[:n]
+
+    def add_extra_offsets(self, batch: "TileBatch", var_size, status: bool = True, stream=None) -> None:
+        """Tile::add_extra_offset on a device batch of unfiltered offsets tiles
+        (tdbg_add_extra_offsets_async; tiles with an error status untouched)."""
+        import torch
+        vs = torch.from_numpy(np.ascontiguousarray(var_size, dtype=np.uint64).view(np.int64)).to(batch.d_out.device)
+        _, _, pout, posz = batch.ptrs()
+        _check(lib.tdbg_add_extra_offsets_async(self.h, batch.ntiles, pout, posz, vs.data_ptr(),
+                                                batch.d_status.data_ptr() if status else None,
+                                                self._stream(stream)), "tdbg_add_extra_offsets_async")
+        torch.cuda.synchronize(batch.d_out.device)
 
 
 def unfilter_cpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, nthreads: int = 0,
