@@ -53,6 +53,9 @@ CONFIGS = {
     "c5": dict(tiles_per_gpu=12500, variants="active,rand,ramp", dtype="int32",
                workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
                         "64 KiB tiles (1 chunk), device-resident, 100k tiles / 8 GPUs"),
+    "c5big": dict(tiles_per_gpu=200, variants="active", dtype="int32",
+                  workload="C5 pipeline, 4 MiB tiles (64 chunks of 64 KiB), 200 tiles per GPU: "
+                           "chunk-parallel launch (device chunk directory)"),
     # XOR / DELTA / FLOAT_SCALE pipelines (not BASELINE configs; tiles encoded
     # on the device by tdbg_filter_tiles, checked against the values)
     "xor": dict(tiles_per_gpu=10000, variants="sin", dtype="float32",

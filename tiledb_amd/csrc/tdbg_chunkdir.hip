@@ -61,7 +61,7 @@ __global__ void dir_count_kernel(const KParams kp, uint32_t* cnt) {
 constexpr int DIR_NT = 1024;
 
 __global__ void __launch_bounds__(DIR_NT) dir_scan_kernel(const KParams kp, uint32_t* cnt, uint32_t* base,
-                                                          uint32_t cap, uint32_t* total) {
+                                                          uint32_t cap, uint32_t* total, uint64_t* need) {
   __shared__ uint64_t red[DIR_NT / 64];
   __shared__ uint32_t placed;  // records written: the placed tiles are a prefix
   if (threadIdx.x == 0) placed = 0;
@@ -97,7 +97,12 @@ __global__ void __launch_bounds__(DIR_NT) dir_scan_kernel(const KParams kp, uint
   // once a tile overflows every later one does (the bases only grow), so
   // the records [0, placed) are exactly the placed tiles' chunks
   __syncthreads();
-  if (threadIdx.x == 0) *total = placed;
+  if (threadIdx.x == 0) {
+    *total = placed;
+    // the records this launch asked for (host-mapped: the next launch on the
+    // context sizes its directory from it, without a host wait here)
+    if (need && carry > *need) *need = carry;
+  }
   // fused-path counters: every tile the directory accepted; a chunk that
   // falls back later takes its tile out again (tdbg_fast.hip)
   if (kp.stats && (ok_tiles | ok_bytes)) {
@@ -131,11 +136,12 @@ __global__ void dir_fill_kernel(const KParams kp, const uint32_t* cnt, const uin
 
 extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
                                             tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
-                                            hipStream_t stream) {
+                                            uint64_t* need, hipStream_t stream) {
   if (kp->ntiles == 0) return hipSuccess;
   const uint32_t grid = (uint32_t)((kp->ntiles + 255) / 256);
   hipLaunchKernelGGL(tdbg::dir_count_kernel, dim3(grid), dim3(256), 0, stream, *kp, cnt);
-  hipLaunchKernelGGL(tdbg::dir_scan_kernel, dim3(1), dim3(tdbg::DIR_NT), 0, stream, *kp, cnt, base, cap, total);
+  hipLaunchKernelGGL(tdbg::dir_scan_kernel, dim3(1), dim3(tdbg::DIR_NT), 0, stream, *kp, cnt, base, cap, total,
+                     need);
   hipLaunchKernelGGL(tdbg::dir_fill_kernel, dim3(grid), dim3(256), 0, stream, *kp, cnt, base, recs);
   return hipGetLastError();
 }

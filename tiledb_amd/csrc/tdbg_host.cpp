@@ -30,7 +30,7 @@ extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
 extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
 extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
                                             tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
-                                            hipStream_t stream);
+                                            uint64_t* need, hipStream_t stream);
 extern "C" hipError_t tdbg_launch_extra_offset(uint64_t ntiles, uint8_t* const* out, const uint64_t* out_size,
                                                const uint64_t* var_size, const int32_t* status,
                                                hipStream_t stream);
@@ -142,6 +142,10 @@ struct tdbg_context {
   tdbg::ChunkRec* dir_recs = nullptr;
   uint32_t* dir_total = nullptr;
   uint64_t dir_tiles = 0, dir_cap = 0;
+  // records the largest launch so far asked for (host-mapped, written by the
+  // directory pass): later launches size the directory from it
+  volatile uint64_t* dir_need = nullptr;
+  uint64_t* dir_need_dev = nullptr;
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -526,6 +530,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->dir_base) (void)hipFree(c->dir_base);
   if (c->dir_recs) (void)hipFree(c->dir_recs);
   if (c->dir_total) (void)hipFree(c->dir_total);
+  if (c->dir_need) (void)hipHostFree((void*)c->dir_need);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -610,9 +615,22 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // Chunk-parallel: asked for, or fewer tiles than CUs (tiles, not chunks,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
-  const bool chunked = queued && !d_list && ((flags & TDBG_CHUNK_PARALLEL) || ntiles < (uint64_t)c->cus);
+  static const bool tile_mode = getenv("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
+  const bool chunked = queued && !d_list &&
+                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
   if (chunked) {
-    const uint64_t want = std::max<uint64_t>(4 * ntiles, 4096);
+    if (!c->dir_need) {
+      void* h = nullptr;
+      HIP_OK(hipHostMalloc(&h, sizeof(uint64_t), hipHostMallocMapped));
+      c->dir_need = (volatile uint64_t*)h;
+      *c->dir_need = 0;
+      HIP_OK(hipHostGetDevicePointer((void**)&c->dir_need_dev, h, 0));
+    }
+    // 64 chunks per tile (4 MiB tiles of 64 KiB chunks), or what an earlier
+    // launch asked for; a tile whose chunks still do not fit goes to the
+    // general interpreter (correct, slower)
+    const uint64_t asked = *c->dir_need;
+    const uint64_t want = std::max<uint64_t>(std::max<uint64_t>(64 * ntiles, 4096), asked);
     if (ntiles > c->dir_tiles || want > c->dir_cap) {
       HIP_OK(hipStreamSynchronize(stream));  // earlier launches may still read the old directory
       if (ntiles > c->dir_tiles) {
@@ -636,7 +654,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (!c->dir_total) HIP_OK(hipMalloc(&c->dir_total, 4));
     hipError_t e = tdbg_launch_chunk_dir(&kp, c->dir_cnt, c->dir_base, c->dir_recs,
                                          (uint32_t)std::min<uint64_t>(c->dir_cap, 0xffffffffull), c->dir_total,
-                                         stream);
+                                         c->dir_need_dev, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("chunk directory launch: ") + hipGetErrorString(e));
     kp.chunks = c->dir_recs;
     kp.nchunks = c->dir_total;

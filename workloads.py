@@ -340,6 +340,11 @@ def config(name: str):
         "c4": (P(PositiveDeltaFilter(1024), BitWidthReductionFilter(256)), Datatype.UINT64, 8,
                lambda var, k, rng: c4_values(k, rng), c4_tile),
         "c5": (c5_pipeline_bytes(), Datatype.INT32, 4, c5_values, c5_filter_tile),
+        # C5's pipeline over 4 MiB tiles (64 chunks of 64 KiB): the chunk-
+        # parallel launch (device chunk directory) against tile-serial chunks
+        "c5big": (c5_pipeline_bytes(), Datatype.INT32, 4,
+                  lambda var, k, rng: np.concatenate([c5_values(var, 64 * k + i, rng) for i in range(64)]),
+                  c5_multi_tile),
         # XOR / DELTA / FLOAT_SCALE pipelines: tiles are
         # encoded by the device forward path (tile = None; bench.py)
         "xor": (P(XORFilter(), BitWidthReductionFilter(256)), Datatype.FLOAT32, 4,
@@ -400,6 +405,14 @@ def c5_values(variant: str, tile_index: int, rng: np.random.Generator) -> np.nda
             i += n
         return out
     raise ValueError(variant)
+
+
+def c5_multi_tile(values: np.ndarray) -> bytes:
+    """A C5 tile of several 64 KiB chunks: WriterTile's chunking
+    (tile.cc:87-100) cuts the tile at 16,384 int32 values, and each chunk
+    record is the one a single-chunk tile of those values holds."""
+    recs = [c5_filter_tile(values[i:i + TILE_VALUES])[8:] for i in range(0, values.size, TILE_VALUES)]
+    return struct.pack("<Q", len(recs)) + b"".join(recs)
 
 
 def c5_dd_bitsize(values: np.ndarray) -> int:
