@@ -13,7 +13,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin")
+declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin" [c5big]="active")
 for CFG in $CFGS; do
   timeout -k 10 200 python3 -u bench.py --config $CFG --cpu-seconds 5 > $OUT/bench_$CFG.log 2>&1 || { echo "bench $CFG failed"; tail -20 $OUT/bench_$CFG.log; exit 11; }
   tail -1 $OUT/bench_$CFG.log
