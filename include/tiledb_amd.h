@@ -306,6 +306,12 @@ int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
 int tdbg_context_path_stats(const tdbg_context* ctx, uint64_t* fused_tiles,
                             uint64_t* fallback_tiles, uint64_t* general_tiles);
 
+/* Of the fused tiles: how many the streaming kernel for the headline pipeline
+ * [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte integers took
+ * (one 64 KiB chunk, DD bit-packed; tdbg_stream.hip).  The tiles it leaves go
+ * to the fused kernel in the same launch.  Cumulative, synchronizes. */
+int tdbg_context_stream_stats(const tdbg_context* ctx, uint64_t* stream_tiles);
+
 /* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on
  * ctx (fused/general kernel + fixup), from the hipEvents that
  * tdbg_context_time_launches arms.  Un-armed launches record no events: an

@@ -62,6 +62,7 @@ SIGNATURES = {
                                               ctypes.c_uint32, c_i32p, c_vp]),
     "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
     "tdbg_context_path_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p, c_u64p]),
+    "tdbg_context_stream_stats": (ctypes.c_int, [c_vp, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "tdbg_context_time_launches": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
     "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint32,

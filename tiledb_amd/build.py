@@ -19,7 +19,7 @@ ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART_HOST)
 # (source, object name, extra flags)
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
-          ("tdbg_forward.hip", "tdbg_forward", []),
+          ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
           # CPU entry: host-only C++, product and sum rounded separately
           # (FLOAT_SCALE parity with the reference's x86-64 build)
           ("tdbg_cpu.cpp", "tdbg_cpu", ["-ffp-contract=off"])] +

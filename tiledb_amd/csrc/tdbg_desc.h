@@ -56,6 +56,7 @@ enum tdbg_stat_slot : uint32_t {
   TDBG_STAT_FALLBACK = 2,       // tiles the fused kernel declined (re-run by the fixup)
   TDBG_STAT_GENERAL_TILES = 3,  // tiles the general interpreter unfiltered (status OK)
   TDBG_STAT_GENERAL_BYTES = 4,
+  TDBG_STAT_STREAM_TILES = 5,   // of the fused tiles: those the streaming C5 kernel took (tdbg_stream.hip)
   TDBG_STAT_N = 8
 };
 
@@ -111,6 +112,13 @@ struct KParams {
   // *nchunks) replaces the tile loop of the fused kernel
   const ChunkRec* chunks;
   const uint32_t* nchunks;
+  // Streaming C5 kernel (tdbg_stream.hip): the tiles it does not take go to
+  // sq (sq[0] = count, sq[1 + k] = tile index, k < sq_cap); the fused kernel
+  // then runs on that list with its length read on the device (ntiles_dev,
+  // capped by ntiles).
+  uint32_t* sq;
+  uint32_t sq_cap;
+  const uint32_t* ntiles_dev;
   tdbg_plan plan;
 };
 

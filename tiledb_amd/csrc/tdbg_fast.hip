@@ -1957,7 +1957,8 @@ struct PhaseClock {
   }
   __device__ __forceinline__ void flush() {
     if (!out || tid_() != 0) return;
-    for (int k = 0; k < TDBG_PROF_PHASES; k++) out[blockIdx.x * TDBG_PROF_PHASES + k] = acc[k];
+    // slots 8..15 belong to the streaming kernel (tdbg_stream.hip), which runs first
+    for (int k = 0; k < TDBG_PROF_PHASES / 2; k++) out[blockIdx.x * TDBG_PROF_PHASES + k] = acc[k];
   }
 };
 
@@ -2155,7 +2156,11 @@ unfilter_fused_kernel(const KParams kp) {
     return;
   }
   // tiles: all ntiles, or a host-given list (the sync entry's retry)
-  const uint64_t ntl = kp.ntiles;
+  uint64_t ntl = kp.ntiles;
+  if (kp.ntiles_dev) {  // the streaming kernel's queue (tdbg_stream.hip)
+    const uint64_t c = (uint32_t)__builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
+    ntl = c < ntl ? c : ntl;
+  }
   const uint32_t* tl = kp.tile_list;
   uint64_t ok_tiles = 0, ok_bytes = 0;
   TileDesc dn{};

@@ -50,6 +50,8 @@ static hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid, hipSt
   return parts[kp->plan.fast % TDBG_NPART_HOST](kp, grid, stream);
 }
 extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan);
+extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
+extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus);
 
 namespace {
@@ -156,6 +158,9 @@ struct tdbg_context {
   // fused-kernel fallback queue (KParams::fbq): count + status_cap entries,
   // count zeroed on the launch stream before every fused launch
   uint32_t* d_fbq = nullptr;
+  // streaming C5 kernel's queue (KParams::sq): the tiles it leaves to the
+  // fused kernel, count + status_cap entries
+  uint32_t* d_sq = nullptr;
   // device path counters (KParams::stats, TDBG_STAT_*)
   uint64_t* d_stats = nullptr;
   // Launch ordering: scratch slots, the fallback queue and the status /
@@ -222,14 +227,18 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   if (c->d_status) HIP_OK(hipFree(c->d_status));
   if (c->d_need) HIP_OK(hipFree(c->d_need));
   if (c->d_fbq) HIP_OK(hipFree(c->d_fbq));
+  if (c->d_sq) HIP_OK(hipFree(c->d_sq));
   c->d_status = nullptr;
   c->d_need = nullptr;
   c->d_fbq = nullptr;
+  c->d_sq = nullptr;
   c->status_cap = 0;
   HIP_OK(hipMalloc(&c->d_status, n * sizeof(int32_t)));
   HIP_OK(hipMalloc(&c->d_need, n * sizeof(uint64_t)));
   HIP_OK(hipMalloc(&c->d_fbq, (n + 1) * sizeof(uint32_t)));
   HIP_OK(hipMemset(c->d_fbq, 0, sizeof(uint32_t)));
+  HIP_OK(hipMalloc(&c->d_sq, (n + 1) * sizeof(uint32_t)));
+  HIP_OK(hipMemset(c->d_sq, 0, sizeof(uint32_t)));
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -523,6 +532,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_need) (void)hipFree(c->d_need);
   if (c->d_list) (void)hipFree(c->d_list);
   if (c->d_fbq) (void)hipFree(c->d_fbq);
+  if (c->d_sq) (void)hipFree(c->d_sq);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->rscratch) (void)hipFree(c->rscratch);
   if (c->fscratch) (void)hipFree(c->fscratch);
@@ -592,12 +602,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   {
     static const bool prof = getenv("TDBG_PROF") != nullptr;
     if (prof && fast) {
-      if (c->prof_grid < grid) {
+      const uint32_t pgrid = std::max<uint32_t>(grid, tdbg_stream_grid(c->cus));
+      if (c->prof_grid < pgrid) {
         if (c->d_prof) (void)hipFree(c->d_prof);
         c->d_prof = nullptr;
         c->prof_grid = 0;
-        HIP_OK(hipMalloc(&c->d_prof, sizeof(uint64_t) * TDBG_PROF_PHASES * grid));
-        c->prof_grid = grid;
+        HIP_OK(hipMalloc(&c->d_prof, sizeof(uint64_t) * TDBG_PROF_PHASES * pgrid));
+        c->prof_grid = pgrid;
       }
       HIP_OK(hipMemsetAsync(c->d_prof, 0, sizeof(uint64_t) * TDBG_PROF_PHASES * c->prof_grid, stream));
       kp.prof = c->d_prof;
@@ -659,6 +670,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kp.chunks = c->dir_recs;
     kp.nchunks = c->dir_total;
   }
+  // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
+  // integers (fused specs 19/20) first goes through the streaming kernel
+  // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
+  static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
+  const bool streamed = queued && !chunked && !d_list && !no_stream &&
+                        (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
+                        p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
+  if (streamed) HIP_OK(hipMemsetAsync(c->d_sq, 0, sizeof(uint32_t), stream));
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   // Events only on armed launches (tdbg_context_time_launches): an event
   // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
@@ -666,9 +685,22 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   hipError_t e = hipSuccess;
   static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
   static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
-  if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
+  if (streamed) {
+    tdbg::KParams ks = kp;
+    ks.sq = c->d_sq;
+    ks.sq_cap = (uint32_t)ntiles;
+    if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), p->plan.s[2].sgn ? 1 : 0, stream);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+    tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
+    kf.tile_list = c->d_sq + 1;
+    kf.ntiles_dev = c->d_sq;
+    if (!skip_fused) e = tdbg_launch_fast(&kf, grid, stream);
+    if (te) HIP_OK(hipEventRecord(te[1], stream));  // kernel time = both kernels
+  } else {
+    if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
+    if (te) HIP_OK(hipEventRecord(te[1], stream));
+  }
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
-  if (te) HIP_OK(hipEventRecord(te[1], stream));
   if (queued && !skip_fixup) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
@@ -971,6 +1003,15 @@ int tdbg_context_path_stats(const tdbg_context* c, uint64_t* fused_tiles, uint64
   if (fused_tiles) *fused_tiles = h[TDBG_STAT_FUSED_TILES];
   if (fallback_tiles) *fallback_tiles = h[TDBG_STAT_FALLBACK];
   if (general_tiles) *general_tiles = h[TDBG_STAT_GENERAL_TILES];
+  return TDBG_OK;
+}
+
+int tdbg_context_stream_stats(const tdbg_context* c, uint64_t* stream_tiles) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (stream_tiles) *stream_tiles = h[TDBG_STAT_STREAM_TILES];
   return TDBG_OK;
 }
 

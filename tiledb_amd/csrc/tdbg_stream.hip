@@ -1,0 +1,691 @@
+// tdbg_stream.hip -- streaming unfilter kernel for the headline pipeline
+// [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte integers
+// (BASELINE C5: dense int32, one 64 KiB chunk per tile), gfx950.
+//
+// The fused LDS kernel (tdbg_fast.hip) materialises every intermediate of
+// a chunk in LDS: BWR's output (the ~59 KB DoubleDelta stream), then DD's
+// output (the 64 KiB byteshuffled chunk), each written in place behind a
+// workgroup barrier, and the byteshuffle gathers the final bytes from LDS.
+// That needs ~80 KB of LDS per tile (two tiles per CU) and a chain of ~8
+// barrier-separated phases per tile.  Here nothing but the filtered tile
+// (~20 KB) is staged in the workgroup's LDS, so four tiles are in flight per
+// CU, and a tile takes three workgroup barriers:
+//
+//   * Thread ownership follows the OUTPUT.  Byteshuffle⁻¹ of 16,384 int32
+//     builds output unit j (16 bytes, elements 4j..4j+3) from dword j of
+//     each of the four byte planes, i.e. from DoubleDelta values j, 4096+j,
+//     8192+j and 12288+j (byteshuffle_filter.cc:111-166 -> blosc2
+//     unshuffle).  Lane l of wave w owns units [1024w + 16l, +16) and so
+//     decodes four runs of 16 consecutive DD values, one per plane; its
+//     outputs leave registers through v_perm 4x4 byte transposes, straight
+//     to HBM.  No DD output or byteshuffle input ever touches LDS.
+//   * BWR⁻¹ (bit_width_reduction_filter.cc:353-404) is decoded lazily per
+//     wave and per plane: the wave decodes, lane-linearly, the ~1 K dwords
+//     of BWR output its 1,024 DD codes sit in, into a wave-private 4 KiB
+//     scratch (no workgroup barrier: LDS is in order within a wave); every
+//     lane then reads its 19 dwords of the DD bit stream from there.  The
+//     window table (LDS) is built once per tile; every wave scans all window
+//     headers itself, so the only barrier is the one that publishes it.
+//   * DD⁻¹ (dd_compressor.cc:314-404): the lane realigns its 16 codes with
+//     per-lane v_alignbyte/v_alignbit, extracts them at compile-time bit
+//     positions (one instantiation per code width cb = bitsize+1 in 2..31),
+//     and folds them into the affine double-delta aggregate (A = sum dd,
+//     B = sum of running deltas); a DPP wave scan and one LDS exchange of
+//     the 16 (plane, wave) totals give every lane its start state.  Values
+//     0 and 1 (x0, x1 in the DD header) enter the same scan as pseudo codes
+//     x0 and x1 - 2 x0.
+//   * The next tile's image is copied into LDS by LDS-DMA
+//     (global_load_lds_dwordx4, no VGPRs) while the current one computes
+//     its values and stores them.
+//
+// The kernel takes only the tile shape it was built for (one chunk of
+// 65,536 bytes, BWR windows of 8/16-bit or raw int32, DD bitsize 1..30, the
+// exact metadata layout the reference writes, image <= CCAP bytes); any
+// other tile is queued for the fused kernel, which runs on the queue right
+// after (and sends what it declines on to the general interpreter), so the
+// status and bytes of every tile stay the reference's.  Nothing is written
+// to a tile's output before all its checks passed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "../../include/tiledb_amd.h"
+#include "tdbg_desc.h"
+#include "tdbg_device.h"
+
+namespace tdbg {
+namespace stream {
+
+constexpr int NT = 256;              // threads per workgroup (4 wave64)
+constexpr int NWV = NT / 64;
+constexpr uint32_t NV = 16384;       // int32 values per chunk
+constexpr uint32_t CCAP = 22016;     // tile image bytes staged in LDS (16-B window)
+constexpr uint32_t CPAD = 64;        // decode reads past the last window stay inside C
+constexpr uint32_t WSD = 1024;       // scratch dwords per wave (256 16-B units)
+constexpr uint32_t TABN = 256;       // BWR windows per chunk
+
+struct Lds {
+  uint32_t C[(CCAP + CPAD) / 4];
+  uint2 TAB[TABN];                   // {LDS byte address | kind << 16, window minimum}
+  uint32_t WS[NWV][WSD];
+  uint32_t red[4][NWV][2];           // per plane and wave: DD aggregate (A, B)
+};
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u g_u4;
+
+__device__ __forceinline__ uint32_t lane_() {
+  uint32_t l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+__device__ __forceinline__ uint32_t wave_() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+// bytes [o, o + 4) of C (any alignment)
+__device__ __forceinline__ uint32_t c32(const Lds& L, uint32_t o) {
+  const uint32_t* p = L.C + (o >> 2);
+  return __builtin_amdgcn_alignbyte(p[1], p[0], o & 3);
+}
+__device__ __forceinline__ uint32_t c8(const Lds& L, uint32_t o) {
+  return (L.C[o >> 2] >> (8 * (o & 3))) & 0xffu;
+}
+
+// ---------------------------------------------------------------------------
+// tile descriptors and the LDS-DMA of a tile image
+// ---------------------------------------------------------------------------
+struct Desc {
+  uint64_t t, fs, os;
+  const uint8_t* in;
+  uint8_t* out;
+};
+
+// Descriptors of the workgroup's tiles, 64 at a time: lane i holds those of
+// its (base + i)-th tile, loaded once (one HBM latency per 64 tiles instead
+// of one per tile) and read back with v_readlane at a uniform index.  The
+// streaming kernel always runs over all tiles (no tile list).
+struct Batch {
+  uint32_t fs, os;  // saturated at 2^32 - 1 (such a tile neither fits nor has 65,536 bytes)
+  uint64_t in, out;
+};
+__device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl) {
+  const uint64_t j = blockIdx.x + (base + (threadIdx.x & 63)) * (uint64_t)gridDim.x;
+  Batch b{0, 0, 0, 0};
+  if (j < ntl) {
+    const uint64_t fs = kp.in_size[j], os = kp.out_size[j];
+    b.fs = fs < 0xffffffffull ? (uint32_t)fs : 0xffffffffu;
+    b.os = os < 0xffffffffull ? (uint32_t)os : 0xffffffffu;
+    b.in = (uint64_t)kp.in[j];
+    b.out = (uint64_t)kp.out[j];
+  }
+  return b;
+}
+// (the builtin returns int: each half goes through uint32_t, or the low half
+// of a pointer would be sign-extended over the high one)
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t k) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, k);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ Desc batch_get(const Batch& b, uint32_t k, uint64_t t) {
+  Desc d;
+  d.t = t;
+  d.fs = (uint32_t)__builtin_amdgcn_readlane(b.fs, k);
+  d.os = (uint32_t)__builtin_amdgcn_readlane(b.os, k);
+  d.in = (const uint8_t*)rl64(b.in, k);
+  d.out = (uint8_t*)rl64(b.out, k);
+  return d;
+}
+
+// the image [in, in + fs) fits the staging window (16-B aligned units)
+__device__ __forceinline__ bool fits(const Desc& d) {
+  if (d.fs < 20 || d.fs > CCAP) return false;
+  const uint64_t a0 = (uint64_t)d.in & ~15ull, a1 = ((uint64_t)d.in + d.fs + 15) & ~15ull;
+  return a1 - a0 <= CCAP;
+}
+
+// LDS-DMA of the image's 16-B units into C: wave w's instruction r moves
+// units [64 (4r + w), +64), lane-linear in LDS.  Inline asm, not the
+// builtin: the compiler would otherwise wait for the DMA (vmcnt(0), which on
+// gfx950 also drains every store before it) at the next LDS read of any
+// address; here the kernel waits for it explicitly, one tile later (wait_dma).
+__device__ __forceinline__ void dma(Lds& L, const Desc& d) {
+  const uint64_t a0 = (uint64_t)d.in & ~15ull, a1 = ((uint64_t)d.in + d.fs + 15) & ~15ull;
+  const uint32_t n16 = (uint32_t)((a1 - a0) >> 4);
+  const uint32_t w = wave_(), l = lane_();
+  for (uint32_t r = 0; r * NT < n16; r++) {
+    const uint32_t ub = r * NT + 64 * w;  // wave-uniform first unit
+    if (ub + l < n16) {
+      const uint64_t src = a0 + 16ull * (ub + l);
+      const uint32_t dst = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)L.C + 16 * ub);
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %2\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, off\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
+          : "memory");
+    }
+  }
+}
+
+// Workgroup barrier for LDS only: no vmcnt drain (outstanding stores and the
+// next tile's DMA stay in flight); "memory" keeps LDS accesses on their side.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// BWR⁻¹ of one 16-B unit u of the BWR output (dwords 4u..4u+3)
+// ---------------------------------------------------------------------------
+struct Win {
+  uint32_t wsh;    // log2(window bytes / 16)
+  uint32_t wlast;  // nwin - 1
+  uint32_t sh;     // LDS byte alignment of the data section (window data keep it)
+};
+
+template <bool SGN>
+__device__ __forceinline__ uint32_t bfe8(uint32_t x, uint32_t o, uint32_t w) {
+  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
+}
+
+template <bool SGN>
+__device__ __forceinline__ v4u bwr_unit_te(const Lds& L, const Win& W, uint32_t u, uint32_t w, uint2 te) {
+  const uint32_t kind = te.x >> 16;  // 0: 8-bit, 1: 16-bit, 2: raw
+  const uint32_t o = (u - (w << W.wsh)) << 4;
+  uint32_t a = (te.x & 0xffffu) + (o >> (2 - kind));
+  a = a < CCAP + CPAD - 20 ? a : CCAP + CPAD - 20;  // units past the stream: any bytes, in bounds
+  const uint32_t* p = L.C + (a >> 2);
+  const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+  const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, W.sh);
+  const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, W.sh);
+  const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, W.sh);
+  const uint32_t r3 = __builtin_amdgcn_alignbyte(d4, d3, W.sh);
+  const uint32_t mn = te.y;
+  const bool b8 = kind == 0, raw = kind == 2;
+  // element i: 8-bit -> byte i of r0; 16-bit -> half (i & 1) of r(i >> 1)
+  const uint32_t e0 = bfe8<SGN>(r0, 0, b8 ? 8 : 16) + mn;
+  const uint32_t e1 = bfe8<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
+  const uint32_t e2 = bfe8<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
+  const uint32_t e3 = bfe8<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
+  return v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
+}
+
+template <bool SGN>
+__device__ __forceinline__ v4u bwr_unit(const Lds& L, const Win& W, uint32_t u) {
+  uint32_t w = u >> W.wsh;
+  w = w < W.wlast ? w : W.wlast;
+  return bwr_unit_te<SGN>(L, W, u, w, L.TAB[w]);
+}
+
+// all-8-bit fast form (the wave checked every lane's window)
+template <bool SGN>
+__device__ __forceinline__ v4u bwr_unit8(const Lds& L, const Win& W, uint32_t u, uint32_t w, uint2 te) {
+  const uint32_t a = (te.x & 0xffffu) + ((u - (w << W.wsh)) << 2);
+  const uint32_t* p = L.C + (a >> 2);
+  const uint32_t r0 = __builtin_amdgcn_alignbyte(p[1], p[0], W.sh);
+  const uint32_t mn = te.y;
+  return v4u{bfe8<SGN>(r0, 0, 8) + mn, bfe8<SGN>(r0, 8, 8) + mn, bfe8<SGN>(r0, 16, 8) + mn,
+             bfe8<SGN>(r0, 24, 8) + mn};
+}
+
+// ---------------------------------------------------------------------------
+// DD⁻¹ codes of one lane and plane (code width CB = bitsize + 1)
+// ---------------------------------------------------------------------------
+// G: 20 dwords of BWR output starting at dword 8 + 2 * (Ms >> 1), Ms the
+// first MSB-first stream dword needed (p = Ms & 1); n: alignbit amount.
+// The stream's u64 words start at BWR-output byte 34 (two 17-byte DD
+// headers precede them), so word q = bytes [34 + 8q, 42 + 8q): H[x] =
+// alignbyte(G[x+1], G[x], 2) are the dwords at byte offset 2, and the
+// MSB-first dword sequence swaps the halves of every word.
+template <int CB>
+__device__ __forceinline__ void dd_codes(const uint32_t (&G)[20], uint32_t p, uint32_t n, bool first,
+                                         uint32_t x0, uint32_t x1, uint32_t (&xl)[16], uint32_t& Aout,
+                                         uint32_t& Bout) {
+  uint32_t H[18];
+#pragma unroll
+  for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
+  // M_j = p ? H[(j+1)^1] : H[j^1] as a bit select (v_bfi_b32): a plain
+  // ternary lets the optimizer turn the pair into an indexed scratch load
+  const uint32_t pm = 0u - p;
+  uint32_t M[17];
+#pragma unroll
+  for (int j = 0; j < 17; j++) M[j] = (pm & H[(j + 1) ^ 1]) | (~pm & H[j ^ 1]);
+  uint32_t A[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) A[j] = __builtin_amdgcn_alignbit(M[j], M[j + 1], n);
+  constexpr int B = CB - 1;
+  uint32_t drun = 0, xrun = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int pos = i * CB;
+    const int j = pos >> 5, o = pos & 31;
+    const int32_t sg = __builtin_amdgcn_sbfe((int32_t)A[j], 31 - o, 1);
+    const int o1a = o + 1;
+    const int jm = j + (o1a >> 5), o1 = o1a & 31;
+    uint32_t mag;
+    if (o1 + B <= 32) {
+      mag = __builtin_amdgcn_ubfe(A[jm], 32 - o1 - B, B);
+    } else {
+      mag = __builtin_amdgcn_alignbit(A[jm], A[jm + 1], 64 - o1 - B) & ((1u << B) - 1u);
+    }
+    uint32_t dd = (mag ^ (uint32_t)sg) - (uint32_t)sg;
+    if (i == 0) dd = first ? x0 : dd;
+    if (i == 1) dd = first ? x1 - 2u * x0 : dd;
+    drun += dd;
+    xrun += drun;
+    xl[i] = xrun;
+  }
+  Aout = drun;
+  Bout = xrun;
+}
+
+template <int CB>
+__device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uint32_t p, uint32_t n,
+                                            bool first, uint32_t x0, uint32_t x1, uint32_t (&xl)[16],
+                                            uint32_t& A, uint32_t& B) {
+  uint32_t G[20];
+#pragma unroll
+  for (int x = 0; x < 10; x++) {
+    const uint2 v = *(const uint2*)(wsp + g + 2 * x);
+    G[2 * x] = v.x;
+    G[2 * x + 1] = v.y;
+  }
+  dd_codes<CB>(G, p, n, first, x0, x1, xl, A, B);
+}
+
+// ---------------------------------------------------------------------------
+// the kernel
+// ---------------------------------------------------------------------------
+// DD aggregate combine: the block with aggregate (Ap, Bp) precedes `self`
+// (nself codes): B = Bp + nself * Ap + B, A = Ap + A.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nself) {
+  const uint32_t Ap = dpp0<CTRL, ROWS>(A), Bp = dpp0<CTRL, ROWS>(B);
+  B = B + Bp + nself * Ap;
+  A = A + Ap;
+}
+
+#ifndef TDBG_STREAM_OCC
+#define TDBG_STREAM_OCC 3  // waves per SIMD: 64 live DD values per lane need > 128 VGPRs
+#endif
+// Diagnostics (KParams::prof, TDBG_PROF=1): per-workgroup shader-clock
+// cycles per phase in slots 8..15 of the profile rows: 8 wait for the image
+// (B1), 9 headers + window table, 10 B2 + DD header, 11 BWR decode into the
+// wave scratch, 12 DD codes, 13 wave scans, 14 B3, 15 start states, values,
+// stores.
+struct Clock {
+  uint64_t* out;
+  uint64_t t, acc[8];
+  __device__ __forceinline__ void init(uint64_t* o) {
+    out = o;
+    if (!out) return;
+    t = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < 8; k++) acc[k] = 0;
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (!out) return;
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    acc[k - 8] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void flush() {
+    if (!out || threadIdx.x != 0) return;
+    for (int k = 0; k < 8; k++) out[blockIdx.x * TDBG_PROF_PHASES + 8 + k] = acc[k];
+  }
+};
+
+// Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
+// base + i) for the fused kernel, which writes their statuses.  Wave 0.
+__device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, uint32_t base) {
+  const uint32_t l = threadIdx.x & 63;
+  uint32_t b0 = 0;
+  if (l == 0) b0 = atomicAdd(kp.sq, (uint32_t)__builtin_popcountll(mask));
+  b0 = __builtin_amdgcn_readfirstlane(b0);
+  if ((mask >> l) & 1) {
+    const uint32_t k = b0 + (uint32_t)__builtin_popcountll(mask & ((1ull << l) - 1));
+    if (k < kp.sq_cap) kp.sq[1 + k] = (uint32_t)(blockIdx.x + (uint64_t)(base + l) * gridDim.x);
+  }
+}
+
+template <bool SGN, bool NTS>
+__global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(const KParams kp) {
+  __shared__ Lds L;
+  const uint64_t G = gridDim.x;
+  uint64_t ntl = kp.ntiles;
+  if (kp.ntiles_dev) {
+    const uint64_t c = (uint32_t)__builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
+    ntl = c < ntl ? c : ntl;
+  }
+  const uint32_t w = wave_();
+  Clock pc;
+  pc.init(kp.prof);
+  uint64_t ok_tiles = 0, ok_bytes = 0;
+  Desc cur{};
+  bool cur_dma = false;
+  bool stored = false;  // the last iteration issued its 16 output stores after the DMA
+  Batch bt{0, 0, 0, 0};
+  if (blockIdx.x < ntl) {
+    bt = batch_load(kp, 0, ntl);
+    cur = batch_get(bt, 0, blockIdx.x);
+    cur_dma = fits(cur);
+    if (cur_dma) dma(L, cur);
+  }
+  // tiles left to the fused kernel, this batch: bit i = iteration i % 64
+  // (queued with one atomic per workgroup and batch: a single global counter
+  // taking one atomic per tile serialises the whole grid on it)
+  uint64_t dmask = 0;
+  uint32_t it = 0;
+  for (uint64_t j = blockIdx.x; j < ntl; j += G, it++) {
+    const uint64_t jn = j + G;
+    const uint32_t l = lane_();
+    // A tile whose image does not fit is declined without touching LDS (and
+    // without barriers: no wave reads C for it, and the last tile that did
+    // passed B3).
+    bool ok = cur_dma && !(kp.flags & TDBG_TILE_OFFSETS) && cur.os == NV * 4 &&
+              (((uintptr_t)cur.out) & 15) == 0;
+    uint32_t xl[4][16];
+    uint32_t Ae[4], Be[4];
+    if (cur_dma) {
+    // B1: this tile's DMA has landed (vmcnt counts in issue order: the last
+    // iteration's 16 output stores, issued after the DMA, may stay in flight)
+    if (stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    pc.mark(8);
+    // ---- tile + chunk header (Tile::load_chunk_data, tile.cc:280-313) -----
+    // Every read below is issued speculatively (all addresses lie inside C
+    // whatever the bytes say) so the parse is two LDS round trips; the
+    // checks then decide.  BWR md: [u32 orig][u32 nwin] + nwin x [i32 min]
+    // [u8 bits][u32 nbytes] (bit_width_reduction_filter.cc:353-380), then the
+    // compression frame's md (compression_filter.cc:413-486).
+    const uint32_t b = (uint32_t)((uintptr_t)cur.in & 15);
+    const uint32_t m = b + 20;
+    uint32_t ml = 0, fl = 0, dst = 0, nwin = 0, wsh = 0, ws = 0;
+    if (ok) {
+      const uint32_t nlo = c32(L, b), nhi = c32(L, b + 4), orig = c32(L, b + 8);
+      fl = c32(L, b + 12);
+      ml = c32(L, b + 16);
+      const uint32_t Lb = c32(L, m), nwr = c32(L, m + 4), ws0 = c32(L, m + 13);
+      // lane l: window entries 4l..4l+3 = 36 bytes at e0 (e0 & 3 is uniform)
+      const uint32_t e0 = m + 8 + 36 * l;
+      const uint32_t* rp = L.C + (e0 >> 2);
+      uint32_t R[10], E[9];
+#pragma unroll
+      for (int k = 0; k < 10; k++) R[k] = rp[k];
+#pragma unroll
+      for (int k = 0; k < 9; k++) E[k] = __builtin_amdgcn_alignbyte(R[k + 1], R[k], e0 & 3);
+      nwin = nwr < TABN ? nwr : TABN;
+      const uint32_t f = m + 8 + 9 * nwin;
+      const uint32_t d0 = c32(L, f), d1 = c32(L, f + 4), d2 = c32(L, f + 8), d3 = c32(L, f + 12),
+                     d4 = c32(L, f + 16), d5 = c32(L, f + 20);
+      dst = m + ml;
+      ws = nwin > 1 ? ws0 : 256;
+      ok = nlo == 1 && nhi == 0 && orig == NV * 4 && (uint64_t)ml + fl + 20 <= cur.fs && nwr >= 1 &&
+           nwr <= TABN && ml == 8 + 9 * nwr + 24 && d0 == 1 && d1 == 1 && d2 == 8 && d3 == 17 &&
+           d4 == NV * 4 && d5 + 17 == Lb && ws >= 64 && ws <= 4096 && (ws & (ws - 1)) == 0 &&
+           (Lb - 1) / ws + 1 == nwin;
+      wsh = ok ? 31 - __builtin_clz(ws) - 4 : 0;
+      if (ok) {
+        // every wave reads all window headers, so all waves reach the same
+        // verdict and offsets without a barrier
+        uint32_t cs[4], kind[4], mn[4];
+        bool bad = false;
+        auto byte_at = [&](int o) -> uint32_t { return (E[o >> 2] >> (8 * (o & 3))) & 0xffu; };
+        auto dw_at = [&](int o) -> uint32_t {
+          return (o & 3) ? __builtin_amdgcn_alignbyte(E[(o >> 2) + 1], E[o >> 2], o & 3) : E[o >> 2];
+        };
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t wi = 4 * l + q;
+          const uint32_t vmin = dw_at(9 * q), bits = byte_at(9 * q + 4), nb = dw_at(9 * q + 5);
+          const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+          const bool in = wi < nwin;
+          bad |= in && nb != want;
+          const bool raw = bits >= 32 || (nb & 3) != 0;
+          bad |= in && !raw && bits != 8 && bits != 16;
+          kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
+          cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+          mn[q] = raw ? 0 : vmin;
+        }
+        const uint32_t s4 = cs[0] + cs[1] + cs[2] + cs[3];
+        const uint32_t inc = wave_incscan_u32(s4);
+        const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        ok = !__builtin_amdgcn_ballot_w64(bad) && total == fl;
+        if (ok && (l >> 4) == w) {
+          uint32_t off = dst + inc - s4;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            L.TAB[4 * l + q] = make_uint2(off | (kind[q] << 16), mn[q]);
+            off += cs[q];
+          }
+        }
+      }
+    }
+    pc.mark(9);
+    // ok is workgroup-uniform: every wave computed it from the same bytes
+    uint32_t cb = 0, x0 = 0, x1 = 0;
+    Win W{wsh, nwin - 1, dst & 3};
+    if (ok) {
+      lds_barrier();  // B2: window table
+      // DD headers: BWR output bytes [0, 34) = c0 (the byteshuffle md) and c1's
+      // header (dd_compressor.cc:314-345); lanes 0..3 decode units 0..3
+      const v4u h = bwr_unit<SGN>(L, W, l < 4 ? l : 3);
+      auto dw = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(h[k & 3], k >> 2); };
+      auto at = [&](int o) -> uint32_t {
+        return __builtin_amdgcn_alignbyte(dw((o >> 2) + 1), dw(o >> 2), o & 3);
+      };
+      const uint32_t num0lo = at(1), num0hi = at(5), np = at(9), psz = at(13);
+      const uint32_t bs = at(17) & 0xffu, num1lo = at(18), num1hi = at(22);
+      x0 = at(26);
+      x1 = at(30);
+      cb = bs + 1;
+      const uint32_t comp1 = c32(L, m + 8 + 9 * nwin + 20);
+      const uint32_t words = ((NV - 2) * cb + 63) / 64;
+      ok = num0lo == 2 && num0hi == 0 && np == 1 && psz == NV * 4 && bs >= 1 && bs <= 30 &&
+           num1lo == NV && num1hi == 0 && comp1 == 17 + 8 * words;
+    }
+    pc.mark(10);
+    if (ok) {
+      // ---- four planes: BWR⁻¹ into the wave scratch, codes, local scans ---
+      uint32_t* wsp = L.WS[w];
+      // rolled (its body holds the 30-way code-width switch); each plane's
+      // results are copied into fixed registers under a uniform branch
+#pragma nounroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t c0w = 4096 * k + 1024 * (int32_t)w - 2;
+        const int32_t P0 = (c0w + 16 * (int32_t)l) * (int32_t)cb;
+        const int32_t b0 = (P0 + 31) >> 5;
+        const uint32_t n = (uint32_t)(32 * b0 - P0);
+        const int32_t Ms = b0 - 1;
+        const uint32_t p = (uint32_t)Ms & 1u;
+        const int32_t es = 8 + 2 * (Ms >> 1);
+        // the wave's range: lane 0 and lane 63 (monotone in l)
+        const int32_t P00 = c0w * (int32_t)cb, P63 = (c0w + 16 * 63) * (int32_t)cb;
+        const int32_t es0 = 8 + 2 * ((((P00 + 31) >> 5) - 1) >> 1);
+        const int32_t es63 = 8 + 2 * ((((P63 + 31) >> 5) - 1) >> 1);
+        const uint32_t ulo = (uint32_t)es0 >> 2;
+        uint32_t nun = (((uint32_t)es63 + 20 + 3) >> 2) - ulo;  // <= 252 for cb <= 31
+        nun = nun < WSD / 4 ? nun : WSD / 4;                     // (never binds; keeps WS in bounds)
+        __builtin_amdgcn_wave_barrier();
+        // four rounds of 64 units (nun <= 252), batched: every table entry
+        // first, one uniform choice of the unit decoder, then the reads
+        (void)nun;
+        uint32_t uu[4], wc[4];
+        uint2 te[4];
+        bool gen = false;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          uu[r] = ulo + 64 * r + l;
+          const uint32_t wu = uu[r] >> W.wsh;
+          wc[r] = wu < W.wlast ? wu : W.wlast;
+          te[r] = L.TAB[wc[r]];
+          gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
+        }
+        v4u dv[4];
+        if (__builtin_amdgcn_ballot_w64(gen) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; r++) dv[r] = bwr_unit_te<SGN>(L, W, uu[r], wc[r], te[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) *(v4u*)(wsp + 4 * (64 * r + l)) = dv[r];
+        __builtin_amdgcn_wave_barrier();
+        pc.mark(11);
+        const uint32_t g = (uint32_t)es - 4 * ulo;
+        const bool first = k == 0 && w == 0 && l == 0;
+        uint32_t A = 0, B = 0, xt[16];
+        switch (cb) {
+#define TDBG_CB(c) \
+  case c: dd_codes_at<c>(wsp, g, p, n, first, x0, x1, xt, A, B); break;
+          TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
+          TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
+          TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
+          TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
+          TDBG_CB(31)
+#undef TDBG_CB
+          default: break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        pc.mark(12);
+        // inclusive wave scan of the (A, B) aggregates, 16 codes per lane
+        const uint32_t As = A, Bs = B;
+        scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
+        scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
+        scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
+        scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
+        scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
+        scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
+        const uint32_t ae = A - As, be = B - Bs - 16 * (A - As);
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++)
+          if (k == kk) {
+            Ae[kk] = ae;
+            Be[kk] = be;
+#pragma unroll
+            for (int i = 0; i < 16; i++) xl[kk][i] = xt[i];
+          }
+        if (l == 63) {
+          L.red[k][w][0] = A;
+          L.red[k][w][1] = B;
+        }
+        pc.mark(13);
+      }
+    }
+    lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals are in red
+    pc.mark(14);
+    }  // cur_dma
+    if (!ok) dmask |= 1ull << (it % 64);
+    if ((it + 1) % 64 == 0 || jn >= ntl) {
+      if (dmask && w == 0) queue_batch(kp, dmask, it - it % 64);
+      dmask = 0;
+    }
+    if ((it + 1) % 64 == 0 && jn < ntl) bt = batch_load(kp, it + 1, ntl);
+    const Desc nxt = batch_get(bt, (it + 1) % 64, jn);
+    const bool nxt_dma = jn < ntl && fits(nxt);
+    if (nxt_dma) dma(L, nxt);
+    if (ok) {
+      // start state of every (plane, wave) block: 1,024 codes each, in order
+      uint32_t X = 0, D = 0, Xs[4] = {0, 0, 0, 0}, Ds[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int v = 0; v < NWV; v++) {
+          if ((uint32_t)v == w) {
+            Xs[k] = X;
+            Ds[k] = D;
+          }
+          const uint32_t A = L.red[k][v][0], B = L.red[k][v][1];
+          X = X + 1024u * D + B;
+          D = D + A;
+        }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t D0 = Ds[k] + Ae[k];
+        uint32_t t = Xs[k] + 16u * l * Ds[k] + Be[k];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          t += D0;
+          xl[k][i] += t;
+        }
+      }
+      // byteshuffle⁻¹: unit i of the lane = dword i of the four planes,
+      // transposed bytewise (out dword b byte k = plane k value byte b).
+      // The lane's 16 units are 256 contiguous bytes, so lane-strided stores
+      // would touch 64 lines per instruction; they go through the wave's
+      // scratch in 4 rounds of 4 units instead: round r, lane L's unit 4r+j
+      // sits at slot j ^ ((L >> 1) & 3) of its 64-B row (conflict-free
+      // writes), and lane l stores row 16q + l/4, unit l % 4 -- four lanes
+      // per 64-byte piece.
+      uint8_t* o = cur.out + 16u * (1024u * w);
+      uint32_t* wsp = L.WS[w];
+      const uint32_t sw = (l >> 1) & 3;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int i = 4 * r + j;
+          const uint32_t t0 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x05010400u);
+          const uint32_t t1 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x07030602u);
+          const uint32_t t2 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x05010400u);
+          const uint32_t t3 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x07030602u);
+          v4u x = {__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
+                   __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
+          *(v4u*)(wsp + 4 * (4 * l + (j ^ sw))) = x;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t Lr = 16 * q + (l >> 2), jr = l & 3;
+          const v4u x = *(const v4u*)(wsp + 4 * (4 * Lr + (jr ^ ((Lr >> 1) & 3))));
+          g_u4* dstp = (g_u4*)(o + 16u * (16u * Lr + 4u * r + jr));
+          if (NTS) __builtin_nontemporal_store(x, dstp);
+          else *dstp = x;
+        }
+      }
+      ok_tiles++;
+      ok_bytes += cur.os;
+      if (threadIdx.x == 0 && kp.status) kp.status[cur.t] = TDBG_OK;
+    }
+    cur = nxt;
+    cur_dma = nxt_dma;
+    stored = ok;
+    pc.mark(15);
+  }
+  pc.flush();
+  if (kp.stats && threadIdx.x == 0 && ok_tiles) {
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
+  }
+}
+
+}  // namespace stream
+}  // namespace tdbg
+
+// Persistent grid: one workgroup per CU for every TDBG_STREAM_OCC waves per
+// SIMD the registers allow (LDS would hold four).
+extern "C" uint32_t tdbg_stream_grid(int cus) { return (uint32_t)cus * TDBG_STREAM_OCC; }
+
+// Launch: sgn = the BWR stage's integer type is signed.
+extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
+  using namespace tdbg::stream;
+  static const bool nts = getenv("TDBG_STREAM_NT") != nullptr;  // experiment: nontemporal stores
+  auto k = sgn ? (nts ? unfilter_stream_kernel<true, true> : unfilter_stream_kernel<true, false>)
+               : (nts ? unfilter_stream_kernel<false, true> : unfilter_stream_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
+  return hipGetLastError();
+}

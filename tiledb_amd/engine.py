@@ -278,6 +278,12 @@ class Context:
                "tdbg_context_path_stats")
         return int(f.value), int(b.value), int(g.value)
 
+    def stream_tiles(self):
+        """Fused tiles the streaming C5 kernel took, cumulative (synchronizes)."""
+        n = ctypes.c_uint64()
+        _check(lib.tdbg_context_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_stats")
+        return int(n.value)
+
     def stats(self):
         """(tiles_unfiltered, read_unfiltered_byte_num)."""
         t, b = ctypes.c_uint64(), ctypes.c_uint64()

@@ -11,7 +11,7 @@ import workloads as W
 from tiledb_amd import engine
 
 NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c|dd-hdr", "final", "tail", "dd-codes+scan",
-         "p8", "p9", "p10", "p11", "p12", "p13", "p14", "p15"]
+         "S:wait", "S:hdr+tab", "S:B2+ddhdr", "S:bwr-decode", "S:dd-codes", "S:scans", "S:B3", "S:values+stores"]
 _ser, _dt, _cs, _, _ = W.config("c5")
 dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)

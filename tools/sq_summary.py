@@ -13,7 +13,7 @@ def collect(d):
     per = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "unfilter_fused_kernel" not in r["Kernel_Name"]:
+            if os.environ.get("TDBG_KNAME", "unfilter_fused_kernel") not in r["Kernel_Name"]:
                 continue
             key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
             per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
