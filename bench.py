@@ -122,6 +122,7 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
         raise SystemExit(f"device status nonzero: {np.unique(st)}")
     ctx.time_launches(steps)
     fused0, fb0, _ = ctx.path_stats()
+    s0 = ctx.stream_tiles()
     batch.d_status.fill_(-1)
     if dist is not None:
         dist.barrier()
@@ -140,9 +141,10 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     if st.any():
         raise SystemExit(f"timed launches: device status nonzero: {np.unique(st)}")
     fused1, fb1, _ = ctx.path_stats()
+    s1 = ctx.stream_tiles()
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, "cuda")
-    return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0)
+    return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0, s1 - s0)
 
 
 def time_forward(engine, ctx, dp, vals, idx, pool, steps: int, warmup: int, dist):
@@ -312,14 +314,14 @@ def main():
             raise SystemExit(f"{var}: first pass status nonzero: {np.unique(st)}")
         if not ablation:
             verify(batch, vals, idx)
-        elapsed, kern_ms, launch_ms, fused, fallback = time_device(
+        elapsed, kern_ms, launch_ms, fused, fallback, streamed = time_device(
             engine, ctx, dp, batch, args.steps, args.warmup, dist, world)
         if not ablation:
             verify(batch, vals, idx)
         unf = float(sum(vals[i].nbytes for i in idx))
         b_alg = float(sizes.sum()) + unf
         res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
-                        out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback,
+                        out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback, streamed=streamed,
                         packed=packed, offs=offs, sizes=sizes)
         if args.forward and vi == 0 and not ablation and args.config != "fscale":  # (lossy: values differ)
             res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, args.steps, args.warmup, dist)
@@ -365,6 +367,7 @@ def main():
             "filtered_bytes_per_gpu": int(r["sizes"].sum()),
             "fused_tiles_timed": r["fused"],
             "fallback_tiles_timed": r["fallback"],
+            "stream_tiles_timed": r["streamed"],
         },
         "roofline": {
             "bound": "hbm",
@@ -375,7 +378,10 @@ def main():
             "traffic": traffic,
             "traffic_source": f"{TRAFFIC_FILE} (committed rocprofv3 --pmc passes of this workload)"
                               if traffic else None,
-            "kernel": "unfilter_fused_kernel",
+            # kernel_ms: the launch's unfilter kernels on its stream (HIP events):
+            # for C5 the streaming kernel, then the fused kernel on its queue
+            "kernel": ("unfilter_stream_kernel + unfilter_fused_kernel (stream queue)" if r["streamed"]
+                       else "unfilter_fused_kernel"),
             "kernel_ms": round(r["kern_ms"], 4),
             "launch_ms": round(r["launch_ms"], 4),
             "algorithmic_bytes_per_launch": int(r["b_alg"]),
@@ -385,6 +391,7 @@ def main():
         line["config"]["variants"] = {
             v: {"GiBps": round(gibps(res[v]), 2), "roofline_frac": round(frac(res[v]), 4),
                 "kernel_ms": round(res[v]["kern_ms"], 4), "fallback_tiles_timed": res[v]["fallback"],
+                "stream_tiles_timed": res[v]["streamed"],
                 "algorithmic_bytes_per_launch": int(res[v]["b_alg"])}
             for v in variants}
         line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v]) for v in variants), 2)

@@ -322,8 +322,8 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
 // Diagnostics (KParams::prof, TDBG_PROF=1): per-workgroup shader-clock
 // cycles per phase in slots 8..15 of the profile rows: 8 wait for the image
 // (B1), 9 headers + window table, 10 B2 + DD header, 11 BWR decode into the
-// wave scratch, 12 DD codes, 13 wave scans, 14 B3, 15 start states, values,
-// stores.
+// wave scratch, 12 DD codes, 13 wave scans, 14 B3 + next DMA + start states
+// + values, 15 byteshuffle transposes and stores.
 struct Clock {
   uint64_t* out;
   uint64_t t, acc[8];
@@ -358,7 +358,7 @@ __device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, ui
   }
 }
 
-template <bool SGN, bool NTS>
+template <bool SGN, int STM>
 __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(const KParams kp) {
   __shared__ Lds L;
   const uint64_t G = gridDim.x;
@@ -585,7 +585,6 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       }
     }
     lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals are in red
-    pc.mark(14);
     }  // cur_dma
     if (!ok) dmask |= 1ull << (it % 64);
     if ((it + 1) % 64 == 0 || jn >= ntl) {
@@ -621,39 +620,45 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
           xl[k][i] += t;
         }
       }
+      pc.mark(14);
       // byteshuffle⁻¹: unit i of the lane = dword i of the four planes,
       // transposed bytewise (out dword b byte k = plane k value byte b).
       // The lane's 16 units are 256 contiguous bytes, so lane-strided stores
       // would touch 64 lines per instruction; they go through the wave's
-      // scratch in 4 rounds of 4 units instead: round r, lane L's unit 4r+j
-      // sits at slot j ^ ((L >> 1) & 3) of its 64-B row (conflict-free
-      // writes), and lane l stores row 16q + l/4, unit l % 4 -- four lanes
-      // per 64-byte piece.
+      // 4 KiB scratch in four rounds instead: units half u, lanes half h.
+      // Lanes [32h, 32h + 32) put units [8u, 8u + 8) in row l & 31 (128 B,
+      // slot j at j ^ (row & 7): conflict-free), then each store
+      // instruction writes 8 whole 128-B lines (8 lanes per line).
       uint8_t* o = cur.out + 16u * (1024u * w);
       uint32_t* wsp = L.WS[w];
-      const uint32_t sw = (l >> 1) & 3;
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        __builtin_amdgcn_wave_barrier();
+      for (int u = 0; u < 2; u++) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int i = 4 * r + j;
-          const uint32_t t0 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x05010400u);
-          const uint32_t t1 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x07030602u);
-          const uint32_t t2 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x05010400u);
-          const uint32_t t3 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x07030602u);
-          v4u x = {__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
-                   __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
-          *(v4u*)(wsp + 4 * (4 * l + (j ^ sw))) = x;
-        }
-        __builtin_amdgcn_wave_barrier();
+        for (int h = 0; h < 2; h++) {
+          __builtin_amdgcn_wave_barrier();
+          if ((l >> 5) == (uint32_t)h) {  // (transposes under the half mask: no registers held)
+            const uint32_t row = l & 31;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t Lr = 16 * q + (l >> 2), jr = l & 3;
-          const v4u x = *(const v4u*)(wsp + 4 * (4 * Lr + (jr ^ ((Lr >> 1) & 3))));
-          g_u4* dstp = (g_u4*)(o + 16u * (16u * Lr + 4u * r + jr));
-          if (NTS) __builtin_nontemporal_store(x, dstp);
-          else *dstp = x;
+            for (int j = 0; j < 8; j++) {
+              const int i = 8 * u + j;
+              const uint32_t t0 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x05010400u);
+              const uint32_t t1 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x07030602u);
+              const uint32_t t2 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x05010400u);
+              const uint32_t t3 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x07030602u);
+              *(v4u*)(wsp + 4 * (8 * row + (j ^ (row & 7)))) =
+                  v4u{__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
+                      __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint32_t row = 8 * q + (l >> 3), sl = l & 7;
+            const v4u y = *(const v4u*)(wsp + 4 * (8 * row + (sl ^ (row & 7))));
+            g_u4* dstp = (g_u4*)(o + 16u * (16u * (32u * h + row) + 8u * u + sl));
+            if (STM == 1) __builtin_nontemporal_store(y, dstp);
+            else *dstp = y;
+          }
         }
       }
       ok_tiles++;
@@ -683,9 +688,10 @@ extern "C" uint32_t tdbg_stream_grid(int cus) { return (uint32_t)cus * TDBG_STRE
 // Launch: sgn = the BWR stage's integer type is signed.
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
   using namespace tdbg::stream;
-  static const bool nts = getenv("TDBG_STREAM_NT") != nullptr;  // experiment: nontemporal stores
-  auto k = sgn ? (nts ? unfilter_stream_kernel<true, true> : unfilter_stream_kernel<true, false>)
-               : (nts ? unfilter_stream_kernel<false, true> : unfilter_stream_kernel<false, false>);
+  // experiment switch: 0 plain stores (default), 1 nontemporal stores
+  static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 0;
+  auto k = sgn ? (stm == 1 ? unfilter_stream_kernel<true, 1> : unfilter_stream_kernel<true, 0>)
+               : (stm == 1 ? unfilter_stream_kernel<false, 1> : unfilter_stream_kernel<false, 0>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
   return hipGetLastError();
 }

@@ -11,7 +11,7 @@ import workloads as W
 from tiledb_amd import engine
 
 NAMES = ["wait", "headers", "stage-a", "stage-b", "stage-c|dd-hdr", "final", "tail", "dd-codes+scan",
-         "S:wait", "S:hdr+tab", "S:B2+ddhdr", "S:bwr-decode", "S:dd-codes", "S:scans", "S:B3", "S:values+stores"]
+         "S:wait", "S:hdr+tab", "S:B2+ddhdr", "S:bwr-decode", "S:dd-codes", "S:scans", "S:B3+dma+values", "S:transpose+stores"]
 _ser, _dt, _cs, _, _ = W.config("c5")
 dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)

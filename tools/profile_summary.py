@@ -1,5 +1,5 @@
-"""Summary of tools/profile_all.sh: per (config, variant) the fused kernel's
-rocprofv3 kernel-trace average over the timed launches, per-launch HBM
+"""Summary of tools/profile_all.sh: per (config, variant) the unfilter kernels'
+(streaming + fused on its queue for C5, else fused) rocprofv3 kernel-trace average over the timed launches, per-launch HBM
 traffic from the --pmc passes (KiB -> bytes; FETCH_SIZE doubled for gfx950
 16-B/lane streaming reads, MI355X_MICROARCH.md "HBM"), the algorithmic bytes
 and roofline fraction from the bench line of the same workload."""
@@ -13,22 +13,43 @@ import sys
 PEAK = 8000.0
 
 
+KERNELS = ("unfilter_stream_kernel", "unfilter_fused_kernel")
+
+
+def _launches(items):
+    """items: (order key, kernel name, value) of the unfilter kernels.  A launch
+    is the streaming kernel plus the fused kernel on its queue (C5), or the
+    fused kernel alone; values of one launch are summed."""
+    out, open_stream = [], False
+    for _, name, v in sorted(items):
+        if "unfilter_stream_kernel" in name:
+            out.append(v)
+            open_stream = True
+        elif open_stream:
+            out[-1] += v
+            open_stream = False
+        else:
+            out.append(v)
+    return out
+
+
 def pmc(d, counter):
     per = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "unfilter_fused_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                k = r.get("Dispatch_Id") or r.get("Correlation_Id")
-                per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
-    return list(per.values())
+            if any(k in r["Kernel_Name"] for k in KERNELS) and r["Counter_Name"] == counter:
+                k = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+                name, v = per.get(k, (r["Kernel_Name"], 0.0))
+                per[k] = (name, v + float(r["Counter_Value"]))
+    return _launches([(k, n, v) for k, (n, v) in per.items()])
 
 
 def trace(d):
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-        rows += [r for r in csv.DictReader(open(f)) if "unfilter_fused_kernel" in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+        rows += [r for r in csv.DictReader(open(f)) if any(k in r["Kernel_Name"] for k in KERNELS)]
+    return _launches([(int(r["Start_Timestamp"]), r["Kernel_Name"],
+                       (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in rows])
 
 
 def stats(d):
@@ -53,7 +74,7 @@ def main(out):
             d = trace(os.path.join(out, f"trace_{cfg}_{v}"))
             if len(d) >= 24:
                 timed = d[-20:]  # sync pass + warmup first, then the 20 timed launches
-                e["rocprof_fused_kernel_avg_us"] = round(statistics.mean(timed), 2)
+                e["rocprof_unfilter_kernels_avg_us"] = round(statistics.mean(timed), 2)
             f = pmc(os.path.join(out, f"pmc_{cfg}_{v}_FETCH_SIZE"), "FETCH_SIZE")
             w = pmc(os.path.join(out, f"pmc_{cfg}_{v}_WRITE_SIZE"), "WRITE_SIZE")
             if f and w:
@@ -69,8 +90,8 @@ def main(out):
             b_alg = (variants[v] or {}).get("algorithmic_bytes_per_launch") or \
                 line["roofline"]["algorithmic_bytes_per_launch"]
             res[h]["algorithmic_bytes_per_launch"] = b_alg
-            if "rocprof_fused_kernel_avg_us" in res[h]:
-                ach = b_alg / (res[h]["rocprof_fused_kernel_avg_us"] * 1e-6) / 1e9
+            if "rocprof_unfilter_kernels_avg_us" in res[h]:
+                ach = b_alg / (res[h]["rocprof_unfilter_kernels_avg_us"] * 1e-6) / 1e9
                 res[h]["rocprof_achieved_GBps"] = round(ach, 1)
                 res[h]["rocprof_roofline_frac"] = round(ach / PEAK, 4)
             if "hbm_bytes_per_launch" in res[h]:
