@@ -143,7 +143,7 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     fused1, fb1, _ = ctx.path_stats()
     s1 = ctx.stream_tiles()
     if dist is not None:
-        elapsed = max_over_ranks(dist, elapsed, "cuda")
+        elapsed = max_over_ranks(dist, elapsed, DIST_DEV)
     return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0, s1 - s0)
 
 
@@ -191,9 +191,14 @@ def time_forward(engine, ctx, dp, vals, idx, pool, steps: int, warmup: int, dist
             if host[o:o + int(lens[k])].tobytes() != bytes(pool[idx[k]]):
                 raise SystemExit(f"forward: tile {k} differs from the encoder's filtered bytes")
     if dist is not None:
-        elapsed = max_over_ranks(dist, elapsed, "cuda")
+        elapsed = max_over_ranks(dist, elapsed, DIST_DEV)
     b_alg = float(fb.in_size.sum() + lens.sum())
     return elapsed, kern_ms, b_alg, float(fb.in_size.sum())
+
+
+# Collective device: "cuda" under RCCL; TDBG_DIST_BACKEND=gloo (a rehearsal of
+# the multi-rank control flow with several ranks on one GPU) reduces on the CPU.
+DIST_DEV = "cuda"
 
 
 def max_over_ranks(dist, x: float, device: str) -> float:
@@ -289,8 +294,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist_mod
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        global DIST_DEV
+        if os.environ.get("TDBG_DIST_BACKEND", "nccl") == "gloo":
+            # rehearsal: ranks may share a GPU (the box has one); same barrier
+            # and max-over-ranks timing, reduced on the CPU
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist_mod.init_process_group("gloo")
+            DIST_DEV = "cpu"
+        else:
+            torch.cuda.set_device(local)
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = dist_mod
     else:
         torch.cuda.set_device(0)
@@ -301,12 +314,12 @@ def main():
     ntiles = args.tiles_per_gpu or cfg["tiles_per_gpu"]
     ser, dt, cs, _, _ = W.config(args.config)
     dp = engine.DevicePipeline(ser, 23, int(dt), cs)
-    ctx = engine.Context(local)
+    ctx = engine.Context(torch.cuda.current_device())  # this rank's GPU (set above)
     variants = [v for v in (args.variants or cfg["variants"]).split(",") if v]
     res = {}
     for vi, var in enumerate(variants):
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
-            engine, args.config, var, ntiles, args.unique, local, seed=5 + 1000 * rank + vi,
+            engine, args.config, var, ntiles, args.unique, torch.cuda.current_device(), seed=5 + 1000 * rank + vi,
             align=args.align, ctx=ctx, dp=dp)
         ablation = bool(os.environ.get("TDBG_DEBUG_STOP"))  # timing-only: outputs unchecked
         st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
@@ -453,7 +466,7 @@ def e2e(engine, ctx, dp, packed, offs, sizes, out_bytes, args, dist=None, world=
     el = time.perf_counter() - t0
     assert not st.any()
     if dist is not None:
-        el = max_over_ranks(dist, el, "cuda")
+        el = max_over_ranks(dist, el, DIST_DEV)
     return round(world * reps * n * out_bytes / el / 2**30, 2)
 
 

@@ -3,9 +3,10 @@
 The path shards: each rank unfilters a contiguous,
 byte-balanced range of tiles (tdbg_shard_tiles) with no collective on the
 data path; the only collectives are the bench's barrier and max-over-ranks
-timing.  Here each rank checks its shard with the CPU oracle (test
-infrastructure), and rank 0 verifies that the gathered shards reproduce the
-single-process result tile for tile.
+timing.  Here each rank unfilters its shard with the product's C++ CPU entry
+(tdbg_unfilter_tiles_cpu, the same C-ABI the GPU ranks drive), checks every
+tile against the generator's source values, and rank 0 verifies that the
+gathered shards cover every tile exactly once.
 """
 from __future__ import annotations
 
@@ -44,20 +45,23 @@ def _worker(rank: int, world: int, port: int, q):
     try:
         import bench
         import workloads as W
-        from oracle import oracle as O
+        from tiledb_amd import engine
         from tiledb_amd.engine import shard_tiles
         tiles, vals = _tiles()
         isz = np.array([len(t) for t in tiles], dtype=np.uint64)
         osz = np.full(len(tiles), W.TILE_BYTES, dtype=np.uint64)
         cuts = shard_tiles(isz, osz, world)
         lo, hi = int(cuts[rank]), int(cuts[rank + 1])
-        op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+        dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
+        bufs = [np.frombuffer(tiles[i], dtype=np.uint8).copy() for i in range(lo, hi)]
+        outs = [np.zeros(W.TILE_BYTES, dtype=np.uint8) for _ in range(lo, hi)]
+        st = engine.unfilter_cpu(dp, [b.ctypes.data for b in bufs], isz[lo:hi],
+                                 [o.ctypes.data for o in outs], osz[lo:hi], nthreads=2)
+        assert not st.any()
         digests = np.zeros(len(tiles), dtype=np.int64)
-        for i in range(lo, hi):
-            rc, out = op.unfilter_tile(tiles[i], W.TILE_BYTES)
-            assert rc == 0
-            assert np.array_equal(out, vals[i].view(np.uint8))
-            digests[i] = int(np.frombuffer(out, dtype=np.uint32).astype(np.uint64).sum()) + 1
+        for k, i in enumerate(range(lo, hi)):
+            assert np.array_equal(outs[k], vals[i].view(np.uint8))
+            digests[i] = int(np.frombuffer(outs[k], dtype=np.uint32).astype(np.uint64).sum()) + 1
         t = torch.from_numpy(digests)
         dist.all_reduce(t)  # disjoint shards: the sum is a gather
         slow = bench.max_over_ranks(dist, float(rank + 1), "cpu")
@@ -72,10 +76,7 @@ def _worker(rank: int, world: int, port: int, q):
 def test_two_rank_shards_cover_every_tile_once():
     import sys
     sys.path.insert(0, ROOT)
-    import workloads as W
-    from oracle import oracle as O
-    O.build()
-    from tiledb_amd import _native  # noqa: F401  (shard_tiles needs the library)
+    from tiledb_amd import _native  # noqa: F401  (the ranks drive the library)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -89,9 +90,6 @@ def test_two_rank_shards_cover_every_tile_once():
         assert p.exitcode == 0
     tiles, vals = _tiles()
     assert cuts[0] == 0 and cuts[-1] == len(tiles) and cuts[0] < cuts[1] < cuts[2]
-    op = O.OraclePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
-    for i, tile in enumerate(tiles):
-        rc, out = op.unfilter_tile(tile, W.TILE_BYTES)
-        assert rc == 0
-        assert digests[i] == int(np.frombuffer(out, dtype=np.uint32).astype(np.uint64).sum()) + 1
+    for i in range(len(tiles)):
+        assert digests[i] == int(vals[i].view(np.uint32).astype(np.uint64).sum()) + 1
     assert slow == 2.0
