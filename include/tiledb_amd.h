@@ -320,10 +320,12 @@ int tdbg_context_last_kernel_ms(tdbg_context* ctx, float* ms);
 
 /* Per-launch device timing for benchmarks: arm event recording for the next
  * n tdbg_unfilter_tiles_* launches on ctx, then read them back (waits for the
- * last armed launch).  A launch is up to two kernels on one stream: the
- * fused LDS kernel (or the general kernel), then the fallback fixup.
- * kernel_ms[i] = the fused/general kernel of launch i, total_ms[i] = all of
- * the launch.  Outputs may be NULL; reading disarms. */
+ * last armed launch).  A launch is up to three kernels on one stream: for the
+ * headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte integers the
+ * streaming kernel and the fused kernel on the tiles it left, otherwise the
+ * fused LDS kernel (or the general kernel); then the fallback fixup.
+ * kernel_ms[i] = the unfilter kernel(s) of launch i before the fixup,
+ * total_ms[i] = all of the launch.  Outputs may be NULL; reading disarms. */
 int tdbg_context_time_launches(tdbg_context* ctx, uint32_t n);
 int tdbg_context_launch_times(tdbg_context* ctx, float* kernel_ms, float* total_ms,
                               uint32_t cap, uint32_t* count);
