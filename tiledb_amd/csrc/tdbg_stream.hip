@@ -69,6 +69,7 @@ struct Lds {
   uint2 TAB[TABN];                   // {LDS byte address | kind << 16, window minimum}
   uint32_t WS[NWV][WSD];
   uint32_t red[4][NWV][2];           // per plane and wave: DD aggregate (A, B)
+  uint64_t clk[8];                   // diagnostics: phase clocks (TDBG_PROF)
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -317,7 +318,7 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
 }
 
 #ifndef TDBG_STREAM_OCC
-#define TDBG_STREAM_OCC 3  // waves per SIMD: 64 live DD values per lane need > 128 VGPRs
+#define TDBG_STREAM_OCC 4  // waves per SIMD = workgroups per CU (128 VGPRs, 40.7 KB LDS)
 #endif
 // Diagnostics (KParams::prof, TDBG_PROF=1): per-workgroup shader-clock
 // cycles per phase in slots 8..15 of the profile rows: 8 wait for the image
@@ -326,17 +327,20 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
 // + values, 15 byteshuffle transposes and stores.
 struct Clock {
   uint64_t* out;
-  uint64_t t, acc[8];
-  __device__ __forceinline__ void init(uint64_t* o) {
+  uint64_t* acc;  // 8 accumulators in the workgroup's LDS (no SGPRs held for them)
+  uint64_t t;
+  __device__ __forceinline__ void init(uint64_t* o, uint64_t* lds_acc) {
     out = o;
+    acc = lds_acc;
     if (!out) return;
     t = __builtin_amdgcn_s_memtime();
-    for (int k = 0; k < 8; k++) acc[k] = 0;
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 8; k++) acc[k] = 0;
   }
   __device__ __forceinline__ void mark(int k) {
     if (!out) return;
     const uint64_t n = __builtin_amdgcn_s_memtime();
-    acc[k - 8] += n - t;
+    if (threadIdx.x == 0) acc[k - 8] += n - t;
     t = n;
   }
   __device__ __forceinline__ void flush() {
@@ -344,6 +348,93 @@ struct Clock {
     for (int k = 0; k < 8; k++) out[blockIdx.x * TDBG_PROF_PHASES + 8 + k] = acc[k];
   }
 };
+
+// The four planes of one tile for one wave (code width CB): BWR⁻¹ of the
+// wave's range into its scratch, the lane's 16 codes straight into xl[k],
+// the local affine scan and the DPP wave scan; the wave totals go to red.
+template <int CB, bool SGN>
+__device__ __forceinline__ void planes(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
+                                       uint32_t (&xl)[4][16], Clock& pc) {
+  uint32_t* wsp = L.WS[w];
+  constexpr int32_t cb = CB;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int32_t c0w = 4096 * k + 1024 * (int32_t)w - 2;
+    const int32_t P0 = (c0w + 16 * (int32_t)l) * cb;
+    const int32_t b0 = (P0 + 31) >> 5;
+    const uint32_t n = (uint32_t)(32 * b0 - P0);
+    const int32_t Ms = b0 - 1;
+    const uint32_t p = (uint32_t)Ms & 1u;
+    const int32_t es = 8 + 2 * (Ms >> 1);
+    // the wave's range starts at lane 0's first dword
+    const int32_t P00 = c0w * cb;
+    const int32_t es0 = 8 + 2 * ((((P00 + 31) >> 5) - 1) >> 1);
+    const uint32_t ulo = (uint32_t)es0 >> 2;
+    __builtin_amdgcn_wave_barrier();
+    // four rounds of 64 units (the wave needs <= 252 for cb <= 31), batched:
+    // every table entry first, one uniform choice of the unit decoder, then
+    // the reads
+    uint32_t uu[4], wc[4];
+    uint2 te[4];
+    bool gen = false;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      uu[r] = ulo + 64 * r + l;
+      const uint32_t wu = uu[r] >> W.wsh;
+      wc[r] = wu < W.wlast ? wu : W.wlast;
+      te[r] = L.TAB[wc[r]];
+      gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
+    }
+    v4u dv[4];
+    if (__builtin_amdgcn_ballot_w64(gen) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
+    } else {
+      // (rare: one unit at a time, so the general decoder's temporaries do
+      // not set the kernel's register count)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        dv[r] = bwr_unit_te<SGN>(L, W, uu[r], wc[r], te[r]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) *(v4u*)(wsp + 4 * (64 * r + l)) = dv[r];
+    __builtin_amdgcn_wave_barrier();
+    pc.mark(11);
+    const uint32_t g = (uint32_t)es - 4 * ulo;
+    const bool first = k == 0 && w == 0 && l == 0;
+    uint32_t A = 0, B = 0;
+    dd_codes_at<CB>(wsp, g, p, n, first, x0, x1, xl[k], A, B);
+    __builtin_amdgcn_wave_barrier();
+    pc.mark(12);
+    // inclusive wave scan of the (A, B) aggregates, 16 codes per lane
+    const uint32_t As = A, Bs = B;
+    scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
+    scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
+    scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
+    scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
+    scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
+    scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
+    // fold the lane's exclusive wave prefix (Ae, Be) into its values now:
+    // x_i = Xs + (16 l + i + 1) Ds + [Be + (i + 1) Ae + xl_i], with (Xs, Ds)
+    // the state at the start of the (plane, wave) block
+    {
+      const uint32_t ae = A - As, be = B - Bs - 16 * (A - As);
+      uint32_t t = be;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        t += ae;
+        xl[k][i] += t;
+      }
+    }
+    if (l == 63) {
+      L.red[k][w][0] = A;
+      L.red[k][w][1] = B;
+    }
+    pc.mark(13);
+  }
+}
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
 // base + i) for the fused kernel, which writes their statuses.  Wave 0.
@@ -369,7 +460,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
   }
   const uint32_t w = wave_();
   Clock pc;
-  pc.init(kp.prof);
+  pc.init(kp.prof, L.clk);
   uint64_t ok_tiles = 0, ok_bytes = 0;
   Desc cur{};
   bool cur_dma = false;
@@ -395,7 +486,6 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     bool ok = cur_dma && !(kp.flags & TDBG_TILE_OFFSETS) && cur.os == NV * 4 &&
               (((uintptr_t)cur.out) & 15) == 0;
     uint32_t xl[4][16];
-    uint32_t Ae[4], Be[4];
     if (cur_dma) {
     // B1: this tile's DMA has landed (vmcnt counts in issue order: the last
     // iteration's 16 output stores, issued after the DMA, may stay in flight)
@@ -498,90 +588,18 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     pc.mark(10);
     if (ok) {
       // ---- four planes: BWR⁻¹ into the wave scratch, codes, local scans ---
-      uint32_t* wsp = L.WS[w];
-      // rolled (its body holds the 30-way code-width switch); each plane's
-      // results are copied into fixed registers under a uniform branch
-#pragma nounroll
-      for (int k = 0; k < 4; k++) {
-        const int32_t c0w = 4096 * k + 1024 * (int32_t)w - 2;
-        const int32_t P0 = (c0w + 16 * (int32_t)l) * (int32_t)cb;
-        const int32_t b0 = (P0 + 31) >> 5;
-        const uint32_t n = (uint32_t)(32 * b0 - P0);
-        const int32_t Ms = b0 - 1;
-        const uint32_t p = (uint32_t)Ms & 1u;
-        const int32_t es = 8 + 2 * (Ms >> 1);
-        // the wave's range: lane 0 and lane 63 (monotone in l)
-        const int32_t P00 = c0w * (int32_t)cb, P63 = (c0w + 16 * 63) * (int32_t)cb;
-        const int32_t es0 = 8 + 2 * ((((P00 + 31) >> 5) - 1) >> 1);
-        const int32_t es63 = 8 + 2 * ((((P63 + 31) >> 5) - 1) >> 1);
-        const uint32_t ulo = (uint32_t)es0 >> 2;
-        uint32_t nun = (((uint32_t)es63 + 20 + 3) >> 2) - ulo;  // <= 252 for cb <= 31
-        nun = nun < WSD / 4 ? nun : WSD / 4;                     // (never binds; keeps WS in bounds)
-        __builtin_amdgcn_wave_barrier();
-        // four rounds of 64 units (nun <= 252), batched: every table entry
-        // first, one uniform choice of the unit decoder, then the reads
-        (void)nun;
-        uint32_t uu[4], wc[4];
-        uint2 te[4];
-        bool gen = false;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          uu[r] = ulo + 64 * r + l;
-          const uint32_t wu = uu[r] >> W.wsh;
-          wc[r] = wu < W.wlast ? wu : W.wlast;
-          te[r] = L.TAB[wc[r]];
-          gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
-        }
-        v4u dv[4];
-        if (__builtin_amdgcn_ballot_w64(gen) == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; r++) dv[r] = bwr_unit_te<SGN>(L, W, uu[r], wc[r], te[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) *(v4u*)(wsp + 4 * (64 * r + l)) = dv[r];
-        __builtin_amdgcn_wave_barrier();
-        pc.mark(11);
-        const uint32_t g = (uint32_t)es - 4 * ulo;
-        const bool first = k == 0 && w == 0 && l == 0;
-        uint32_t A = 0, B = 0, xt[16];
-        switch (cb) {
+      // one instantiation per code width: the plane loop unrolls and every
+      // plane's codes land directly in their value registers
+      switch (cb) {
 #define TDBG_CB(c) \
-  case c: dd_codes_at<c>(wsp, g, p, n, first, x0, x1, xt, A, B); break;
-          TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
-          TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
-          TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
-          TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
-          TDBG_CB(31)
+  case c: planes<c, SGN>(L, W, w, l, x0, x1, xl, pc); break;
+        TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
+        TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
+        TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
+        TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
+        TDBG_CB(31)
 #undef TDBG_CB
-          default: break;
-        }
-        __builtin_amdgcn_wave_barrier();
-        pc.mark(12);
-        // inclusive wave scan of the (A, B) aggregates, 16 codes per lane
-        const uint32_t As = A, Bs = B;
-        scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
-        scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
-        scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
-        scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
-        scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
-        scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
-        const uint32_t ae = A - As, be = B - Bs - 16 * (A - As);
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++)
-          if (k == kk) {
-            Ae[kk] = ae;
-            Be[kk] = be;
-#pragma unroll
-            for (int i = 0; i < 16; i++) xl[kk][i] = xt[i];
-          }
-        if (l == 63) {
-          L.red[k][w][0] = A;
-          L.red[k][w][1] = B;
-        }
-        pc.mark(13);
+        default: break;
       }
     }
     lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals are in red
@@ -606,17 +624,18 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
             Xs[k] = X;
             Ds[k] = D;
           }
-          const uint32_t A = L.red[k][v][0], B = L.red[k][v][1];
+          // uniform: scalar registers, not 32 VGPRs of LDS reads
+          const uint32_t A = __builtin_amdgcn_readfirstlane(L.red[k][v][0]);
+          const uint32_t B = __builtin_amdgcn_readfirstlane(L.red[k][v][1]);
           X = X + 1024u * D + B;
           D = D + A;
         }
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const uint32_t D0 = Ds[k] + Ae[k];
-        uint32_t t = Xs[k] + 16u * l * Ds[k] + Be[k];
+        uint32_t t = Xs[k] + 16u * l * Ds[k];
 #pragma unroll
         for (int i = 0; i < 16; i++) {
-          t += D0;
+          t += Ds[k];
           xl[k][i] += t;
         }
       }
@@ -657,7 +676,9 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
             const v4u y = *(const v4u*)(wsp + 4 * (8 * row + (sl ^ (row & 7))));
             g_u4* dstp = (g_u4*)(o + 16u * (16u * (32u * h + row) + 8u * u + sl));
             if (STM == 1) __builtin_nontemporal_store(y, dstp);
-            else *dstp = y;
+            else if (STM == 3) {  // timing ablation: no stores (output left unwritten)
+              if (y.x == 0x9e3779b9u && y.y == 0x7f4a7c15u) *dstp = y;
+            } else *dstp = y;
           }
         }
       }
@@ -688,9 +709,10 @@ extern "C" uint32_t tdbg_stream_grid(int cus) { return (uint32_t)cus * TDBG_STRE
 // Launch: sgn = the BWR stage's integer type is signed.
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
   using namespace tdbg::stream;
-  // experiment switch: 0 plain stores (default), 1 nontemporal stores
+  // experiment switch: 0 plain stores (default), 1 nontemporal stores, 3 no stores (timing)
   static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 0;
-  auto k = sgn ? (stm == 1 ? unfilter_stream_kernel<true, 1> : unfilter_stream_kernel<true, 0>)
+  auto k = sgn ? (stm == 1 ? unfilter_stream_kernel<true, 1>
+                  : stm == 3 ? unfilter_stream_kernel<true, 3> : unfilter_stream_kernel<true, 0>)
                : (stm == 1 ? unfilter_stream_kernel<false, 1> : unfilter_stream_kernel<false, 0>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
   return hipGetLastError();
