@@ -161,6 +161,9 @@ struct tdbg_context {
   // streaming C5 kernel's queue (KParams::sq): the tiles it leaves to the
   // fused kernel, count + status_cap entries
   uint32_t* d_sq = nullptr;
+  // d_sq[0] is 0 (the last streamed launch's fixup kernel reset it), so the
+  // next streamed launch needs no memset for it
+  bool sq_clean = true;
   // device path counters (KParams::stats, TDBG_STAT_*)
   uint64_t* d_stats = nullptr;
   // Launch ordering: scratch slots, the fallback queue and the status /
@@ -239,6 +242,7 @@ int ensure_status(tdbg_context* c, uint64_t n) {
   HIP_OK(hipMemset(c->d_fbq, 0, sizeof(uint32_t)));
   HIP_OK(hipMalloc(&c->d_sq, (n + 1) * sizeof(uint32_t)));
   HIP_OK(hipMemset(c->d_sq, 0, sizeof(uint32_t)));
+  c->sq_clean = true;
   c->status_cap = n;
   return TDBG_OK;
 }
@@ -621,14 +625,27 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kp.fbq = c->d_fbq;
     kp.fbq_cap = (uint32_t)ntiles;
   }
-  // the queue starts empty for this launch, whatever ran before on any stream
-  if (queued) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
   // Chunk-parallel: asked for, or fewer tiles than CUs (tiles, not chunks,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
   static const bool tile_mode = getenv("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
   const bool chunked = queued && !d_list &&
                        ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
+  // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
+  // integers (fused specs 19/20) first goes through the streaming kernel
+  // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
+  static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
+  const bool streamed = queued && !chunked && !d_list && !no_stream &&
+                        (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
+                        p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
+  // The fallback queue starts empty for this launch, whatever ran before on
+  // any stream: a memset, or in a streamed launch the streaming kernel's first
+  // thread (it runs before the fused kernel that appends).  The streaming
+  // kernel's own queue count was reset by the last streamed launch's fixup
+  // kernel (or is reset here): two memset launches fewer per C5 launch.
+  if (queued && !streamed) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
+  if (streamed && !c->sq_clean) HIP_OK(hipMemsetAsync(c->d_sq, 0, sizeof(uint32_t), stream));
+  if (streamed) c->sq_clean = false;  // until this launch's fixup is enqueued
   if (chunked) {
     if (!c->dir_need) {
       void* h = nullptr;
@@ -670,14 +687,6 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kp.chunks = c->dir_recs;
     kp.nchunks = c->dir_total;
   }
-  // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
-  // integers (fused specs 19/20) first goes through the streaming kernel
-  // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
-  static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
-  const bool streamed = queued && !chunked && !d_list && !no_stream &&
-                        (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
-                        p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
-  if (streamed) HIP_OK(hipMemsetAsync(c->d_sq, 0, sizeof(uint32_t), stream));
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   // Events only on armed launches (tdbg_context_time_launches): an event
   // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
@@ -707,8 +716,10 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     // with an empty queue every workgroup exits after one load
     tdbg::KParams g = kp;
     g.fixup = 1;
+    g.sq = streamed ? c->d_sq : nullptr;  // the fixup resets the streaming queue's count
     e = tdbg_launch_fixup(&g, std::min<uint32_t>(ggrid, (uint32_t)c->cus), stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
+    if (streamed) c->sq_clean = true;
   }
   if (te) {
     HIP_OK(hipEventRecord(te[2], stream));

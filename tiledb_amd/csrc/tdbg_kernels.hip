@@ -73,6 +73,9 @@ unfilter_general_kernel(const KParams kp) {
 // entry only reads its count (the interpreter's prologue sits behind the call).
 __global__ void __launch_bounds__(GEN_NT)
 unfilter_fixup_kernel(const KParams kp) {
+  // streamed launches: the streaming kernel's queue was consumed by the fused
+  // kernel before this launch started; its count is reset for the next launch
+  if (kp.sq && blockIdx.x == 0 && threadIdx.x == 0) kp.sq[0] = 0;
   const uint32_t queued = kp.fbq[0];
   if (queued == 0) return;
   if (blockIdx.x == 0 && threadIdx.x == 0 && kp.stats)

@@ -458,6 +458,9 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     const uint64_t c = (uint32_t)__builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
     ntl = c < ntl ? c : ntl;
   }
+  // the fused kernel's fallback queue starts empty for this launch (it runs
+  // next on the same stream and is the only one to append)
+  if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const uint32_t w = wave_();
   Clock pc;
   pc.init(kp.prof, L.clk);
