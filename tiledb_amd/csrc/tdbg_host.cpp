@@ -717,7 +717,11 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     tdbg::KParams g = kp;
     g.fixup = 1;
     g.sq = streamed ? c->d_sq : nullptr;  // the fixup resets the streaming queue's count
-    e = tdbg_launch_fixup(&g, std::min<uint32_t>(ggrid, (uint32_t)c->cus), stream);
+    // After a streamed launch the queue holds only tiles both fast kernels
+    // declined (malformed or unusual ones): a small grid, whose dispatch is
+    // most of an empty fixup launch's cost
+    const uint32_t fgrid = std::min<uint32_t>(ggrid, streamed ? 32u : (uint32_t)c->cus);
+    e = tdbg_launch_fixup(&g, fgrid, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
     if (streamed) c->sq_clean = true;
   }
