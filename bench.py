@@ -321,7 +321,9 @@ def main():
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
             engine, args.config, var, ntiles, args.unique, torch.cuda.current_device(), seed=5 + 1000 * rank + vi,
             align=args.align, ctx=ctx, dp=dp)
-        ablation = bool(os.environ.get("TDBG_DEBUG_STOP"))  # timing-only: outputs unchecked
+        # timing-only ablations (outputs unchecked): TDBG_DEBUG_STOP (fused
+        # kernel stages) or TDBG_BENCH_NOVERIFY (e.g. TDBG_RAW_ABL, TDBG_STREAM_STORE=3)
+        ablation = bool(os.environ.get("TDBG_DEBUG_STOP") or os.environ.get("TDBG_BENCH_NOVERIFY"))
         st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
         if st.any():
             raise SystemExit(f"{var}: first pass status nonzero: {np.unique(st)}")

@@ -109,8 +109,10 @@ enum tdbg_status {
   TDBG_E_DD_OVERFLOW = 13,  /* forward only: delta exceeds int64               */
   TDBG_E_DEVICE = 14,       /* HIP runtime error                               */
   TDBG_E_DESCRIPTOR = 15,   /* malformed serialized pipeline                    */
-  TDBG_E_DELTA_TYPE = 16    /* Delta float: "Decompression is not yet supported for
+  TDBG_E_DELTA_TYPE = 16,   /* Delta float: "Decompression is not yet supported for
                                float datatypes." delta_compressor.cc:210-213   */
+  TDBG_E_INTERNAL = 17      /* internal engine error (a device work queue overflowed):
+                               the tile was not unfiltered; never expected   */
 };
 
 /* unfilter flags */
@@ -237,7 +239,10 @@ int tdbg_shard_tiles(uint64_t ntiles, const uint64_t* in_size, const uint64_t* o
 
 /* Multi-GPU host-resident end-to-end: tiles are sharded over devices by
  * contiguous ranges balanced by bytes, one host thread + context per device,
- * no inter-GPU communication. */
+ * no inter-GPU communication.  The per-device contexts (staging, status and
+ * scratch buffers) are kept in a process-wide pool and reused by later calls
+ * (a reader calls this once per batch); tdbg_release_cached_contexts frees
+ * the pooled ones. */
 int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   const uint8_t* const* filtered,
                                   const uint64_t* filtered_size,
@@ -245,6 +250,11 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   const uint64_t* out_size, uint32_t flags,
                                   int32_t* host_status, const int* devices,
                                   int ndevices, uint64_t batch_bytes);
+/* Destroys the contexts the multi-GPU entry keeps for reuse (none is in use
+ * by a running call afterwards only if no call is running). */
+int tdbg_release_cached_contexts(void);
+/* Number of idle pooled contexts (diagnostics / tests). */
+int tdbg_cached_context_count(void);
 
 /* CPU entry: the same batch unfilter on host threads, for
  * host-resident tiles and the CPU baseline.  The work split is the
@@ -306,11 +316,15 @@ int tdbg_context_stats(const tdbg_context* ctx, uint64_t* tiles_unfiltered,
 int tdbg_context_path_stats(const tdbg_context* ctx, uint64_t* fused_tiles,
                             uint64_t* fallback_tiles, uint64_t* general_tiles);
 
-/* Of the fused tiles: how many the streaming kernel for the headline pipeline
- * [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte integers took
- * (one 64 KiB chunk, DD bit-packed; tdbg_stream.hip).  The tiles it leaves go
- * to the fused kernel in the same launch.  Cumulative, synchronizes. */
+/* Of the fused tiles: how many the streaming kernels for the headline
+ * pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte integers
+ * took (one 64 KiB chunk; DD bit-packed: tdbg_stream.hip, DD raw:
+ * tdbg_stream_raw.hip).  The tiles they leave go to the fused kernel in the
+ * same launch.  Cumulative; waits for the context's last launch. */
 int tdbg_context_stream_stats(const tdbg_context* ctx, uint64_t* stream_tiles);
+/* Of those, the tiles the raw-DoubleDelta streaming kernel took (C5 tiles
+ * whose DD stage stored the values raw, tdbg_stream_raw.hip). */
+int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles);
 
 /* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on
  * ctx (fused/general kernel + fixup), from the hipEvents that

@@ -53,6 +53,8 @@ SIGNATURES = {
                                                      ctypes.c_uint32, c_i32p,
                                                      ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                                      ctypes.c_uint64]),
+    "tdbg_release_cached_contexts": (ctypes.c_int, []),
+    "tdbg_cached_context_count": (ctypes.c_int, []),
     "tdbg_unfilter_tiles_cpu": (ctypes.c_int, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
                                                ctypes.c_uint32, c_i32p, ctypes.c_uint32]),
     "tdbg_filtered_bound": (ctypes.c_uint64, [c_vp, ctypes.c_uint64, ctypes.c_uint32]),
@@ -63,6 +65,7 @@ SIGNATURES = {
     "tdbg_context_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p]),
     "tdbg_context_path_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p, c_u64p]),
     "tdbg_context_stream_stats": (ctypes.c_int, [c_vp, c_u64p]),
+    "tdbg_context_stream_raw_stats": (ctypes.c_int, [c_vp, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "tdbg_context_time_launches": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
     "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint32,

@@ -20,13 +20,15 @@ NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART
 # (source, object name, extra flags)
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
           ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
+          ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
           # CPU entry: host-only C++, product and sum rounded separately
           # (FLOAT_SCALE parity with the reference's x86-64 build)
           ("tdbg_cpu.cpp", "tdbg_cpu", ["-ffp-contract=off"])] +
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
 HOST_ONLY = {"tdbg_cpu.cpp"}
-HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h"]
+NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip"}  # checked with -Rpass-analysis
+HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h"]
 
 
 def _deps(src: str):
@@ -70,7 +72,21 @@ def build(force: bool = False, verbose: bool = False) -> str:
     def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.check_call(cmd)
+        src = cmd[cmd.index("-c") + 1]
+        if os.path.basename(src) in NO_SCRATCH:
+            # the streaming kernels count their own vector-memory operations
+            # (s_waitcnt vmcnt(N)): a register spill would add scratch
+            # loads/stores to the count, so the build refuses any
+            r = subprocess.run(cmd + ["-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+            if r.returncode:
+                sys.stderr.write(r.stderr)
+                raise subprocess.CalledProcessError(r.returncode, cmd)
+            bad = [ln for ln in r.stderr.splitlines() if "ScratchSize" in ln and not ln.rstrip().endswith(": 0")
+                   and "[bytes/lane]: 0 " not in ln]
+            if bad:
+                raise RuntimeError(f"{src}: kernels use scratch (counted vmcnt waits would break):\n" + "\n".join(bad))
+        else:
+            subprocess.check_call(cmd)
 
     nproc = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(nproc) as ex:

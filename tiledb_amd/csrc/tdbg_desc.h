@@ -56,7 +56,8 @@ enum tdbg_stat_slot : uint32_t {
   TDBG_STAT_FALLBACK = 2,       // tiles the fused kernel declined (re-run by the fixup)
   TDBG_STAT_GENERAL_TILES = 3,  // tiles the general interpreter unfiltered (status OK)
   TDBG_STAT_GENERAL_BYTES = 4,
-  TDBG_STAT_STREAM_TILES = 5,   // of the fused tiles: those the streaming C5 kernel took (tdbg_stream.hip)
+  TDBG_STAT_STREAM_TILES = 5,   // of the fused tiles: those the streaming C5 kernels took (tdbg_stream*.hip)
+  TDBG_STAT_STREAM_RAW_TILES = 6,  // of those: the raw-DoubleDelta kernel's (tdbg_stream_raw.hip)
   TDBG_STAT_N = 8
 };
 

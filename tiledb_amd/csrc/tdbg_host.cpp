@@ -52,6 +52,8 @@ static hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid, hipSt
 extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan);
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_grid(int cus);
+extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
+extern "C" uint32_t tdbg_stream_raw_grid(int cus);
 extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus);
 
 namespace {
@@ -397,6 +399,7 @@ const char* tdbg_status_str(int s) {
     case TDBG_E_DEVICE: return "HIP runtime error";
     case TDBG_E_DESCRIPTOR: return "Deserialization error; malformed filter pipeline";
     case TDBG_E_DELTA_TYPE: return "Decompression is not yet supported for float datatypes.";
+    case TDBG_E_INTERNAL: return "internal: device work queue overflow";
     default: return "unknown";
   }
 }
@@ -698,8 +701,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     tdbg::KParams ks = kp;
     ks.sq = c->d_sq;
     ks.sq_cap = (uint32_t)ntiles;
-    if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), p->plan.s[2].sgn ? 1 : 0, stream);
+    // the coded-DD kernel takes the tiles of at most its staging cap, the
+    // raw-DD kernel the bigger ones; both queue what they decline
+    const int sgn = p->plan.s[2].sgn ? 1 : 0;
+    if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+    if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
     kf.tile_list = c->d_sq + 1;
     kf.ntiles_dev = c->d_sq;
@@ -835,10 +843,15 @@ int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   return TDBG_OK;
 }
 
+// The counters as of this context's last launch: the copy is ordered on
+// the stream of that launch (every launch of a context is ordered behind the
+// previous one, order_stream), so other contexts and streams of the device
+// keep running.
 static int read_stats(const tdbg_context* c, uint64_t (&h)[TDBG_STAT_N]) {
   HIP_OK(hipSetDevice(c->device));
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  const hipStream_t s = c->last_stream_set ? c->last_stream : nullptr;
+  HIP_OK(hipMemcpyAsync(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
   return TDBG_OK;
 }
 
@@ -852,15 +865,60 @@ static uint64_t fwd_chunk_bound(uint64_t tile_size, uint64_t cell, uint32_t max_
   return std::max<uint64_t>(c, cell ? cell : 1);
 }
 
+// Worst-case filtered size, by walking the pipeline forward over one full
+// chunk with every filter's largest growth: BWR / PD window metadata for
+// one-element windows (bit_width_reduction_filter.cc:218-250: [u32 orig]
+// [u32 nwin] + nwin x [T min][u8 bits][u32 bytes]; positive_delta_filter.cc:
+// 183-205: [u32 nwin] + nwin x [T first][u32 bytes]) adding up over every
+// such stage, shuffle / XOR / FLOAT_SCALE part tables, FLOAT_SCALE's width
+// change, and the compression filters, which fold all earlier metadata into
+// their data (compression_filter.cc:240-301) with DD / DELTA raw fallback
+// headers (dd_compressor.cc:229-261) and RLE's (cell + 2) bytes per cell
+// (rle_compressor.cc:51-101).  Parts per buffer are bounded by kParts.
 uint64_t tdbg_filtered_bound(const tdbg_pipeline* p, uint64_t tile_size, uint32_t max_chunk) {
   if (!p) return 0;
   const uint64_t chunk = fwd_chunk_bound(tile_size, p->cell_size, max_chunk);
-  const uint64_t nch = tile_size / chunk + 2;
-  // per chunk: header, per-filter metadata (windows of >= 1 element: at most
-  // 13 B per element), RLE growth (3x for 1-byte cells), DD/DELTA headers
-  const uint64_t nf = p->filters.size();
-  return 8 + nch * (12 + 64 + 64 * nf) + tile_size * 3 + (tile_size / 2 + 64) * 13 * std::min<uint64_t>(nf, 4) +
-         4096;
+  const uint64_t nch = (tile_size + chunk - 1) / chunk + 1;
+  constexpr uint64_t kParts = 4;
+  uint64_t D = chunk, M = 0, MP = 0;  // data bytes, metadata bytes, metadata buffers
+  for (const Filter& f : p->filters) {
+    const uint64_t ts = dt_size(f.datatype);
+    switch (f.type) {
+      case TDBG_FILTER_BYTESHUFFLE: case TDBG_FILTER_BITSHUFFLE: case TDBG_FILTER_XOR:
+        M += 4 + 8 * kParts;
+        MP++;
+        break;
+      case TDBG_FILTER_SCALE_FLOAT:
+        M += 4 + 8 * kParts;
+        MP++;
+        D = D / (ts ? ts : 1) * std::max<uint64_t>(f.byte_width, 1) + 8;
+        break;
+      case TDBG_FILTER_BIT_WIDTH_REDUCTION:
+        M += 8 * kParts + (D / (ts ? ts : 1) + kParts) * (ts + 5);
+        MP++;
+        break;
+      case TDBG_FILTER_POSITIVE_DELTA:
+        M += 4 * kParts + (D / (ts ? ts : 1) + kParts) * (ts + 4);
+        MP++;
+        break;
+      case TDBG_FILTER_DOUBLE_DELTA: case TDBG_FILTER_DELTA:
+        D = M + D + 64 * (MP + kParts);
+        M = 8 + 8 * (MP + kParts);
+        MP = 1;
+        break;
+      case TDBG_FILTER_RLE: {
+        const uint64_t cs = p->cell_size ? p->cell_size : 1;
+        auto grow = [&](uint64_t x) { return x / cs * (cs + 2) + 2 * (cs + 2); };
+        D = grow(M) + grow(D) + 64 * (MP + kParts);
+        M = 8 + 8 * (MP + kParts);
+        MP = 1;
+        break;
+      }
+      default:
+        break;  // NOOP / pass-through stages; unsupported pipelines never launch
+    }
+  }
+  return 8 + nch * (12 + M + D) + 4096;
 }
 
 static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, const uint8_t* const* d_in,
@@ -1027,6 +1085,15 @@ int tdbg_context_stream_stats(const tdbg_context* c, uint64_t* stream_tiles) {
   int rc = read_stats(c, h);
   if (rc) return rc;
   if (stream_tiles) *stream_tiles = h[TDBG_STAT_STREAM_TILES];
+  return TDBG_OK;
+}
+
+int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (raw_tiles) *raw_tiles = h[TDBG_STAT_STREAM_RAW_TILES];
   return TDBG_OK;
 }
 
@@ -1346,6 +1413,52 @@ int tdbg_shard_tiles(uint64_t ntiles, const uint64_t* in_size, const uint64_t* o
   return TDBG_OK;
 }
 
+}  // extern "C"
+
+// Contexts of the multi-GPU entry, kept across calls: a reader calls it once
+// per batch of tiles, and a fresh context per call would hipMalloc its
+// staging, status and scratch buffers every time.  A context serves one host
+// thread at a time: taken out of the pool for the call, put back after.
+namespace {
+std::mutex g_pool_mu;
+std::vector<tdbg_context*> g_pool;
+
+int pool_acquire(int device, tdbg_context** out) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); i++)
+      if (g_pool[i]->device == device) {
+        *out = g_pool[i];
+        g_pool.erase(g_pool.begin() + (std::ptrdiff_t)i);
+        return TDBG_OK;
+      }
+  }
+  return tdbg_context_create(device, out);
+}
+
+void pool_release(tdbg_context* c) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.push_back(c);
+}
+}  // namespace
+
+extern "C" {
+
+int tdbg_release_cached_contexts(void) {
+  std::vector<tdbg_context*> v;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    v.swap(g_pool);
+  }
+  for (auto c : v) tdbg_context_destroy(c);
+  return TDBG_OK;
+}
+
+int tdbg_cached_context_count(void) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  return (int)g_pool.size();
+}
+
 int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
                                   const uint8_t* const* in, const uint64_t* in_size,
                                   uint8_t* const* out, const uint64_t* out_size, uint32_t flags,
@@ -1364,11 +1477,11 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
       const uint64_t lo = cut[d], hi = cut[d + 1];
       if (hi <= lo) return;
       tdbg_context* c = nullptr;
-      int rc = tdbg_context_create(devices[d], &c);
+      int rc = pool_acquire(devices[d], &c);
       if (rc == TDBG_OK) {
         rc = tdbg_unfilter_tiles_host(c, p, hi - lo, in + lo, in_size + lo, out + lo, out_size + lo,
                                       flags, st.data() + lo, batch_bytes);
-        tdbg_context_destroy(c);
+        pool_release(c);
       }
       rcs[d] = rc;
       if (rc) errs[d] = g_err;

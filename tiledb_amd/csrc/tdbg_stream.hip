@@ -52,6 +52,7 @@
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
 #include "tdbg_device.h"
+#include "tdbg_stream_common.h"
 
 namespace tdbg {
 namespace stream {
@@ -59,7 +60,7 @@ namespace stream {
 constexpr int NT = 256;              // threads per workgroup (4 wave64)
 constexpr int NWV = NT / 64;
 constexpr uint32_t NV = 16384;       // int32 values per chunk
-constexpr uint32_t CCAP = 22016;     // tile image bytes staged in LDS (16-B window)
+constexpr uint32_t CCAP = sc::CODED_CAP;  // tile image bytes staged in LDS (16-B window)
 constexpr uint32_t CPAD = 64;        // decode reads past the last window stay inside C
 constexpr uint32_t WSD = 1024;       // scratch dwords per wave (256 16-B units)
 constexpr uint32_t TABN = 256;       // BWR windows per chunk
@@ -69,20 +70,21 @@ struct Lds {
   uint2 TAB[TABN];                   // {LDS byte address | kind << 16, window minimum}
   uint32_t WS[NWV][WSD];
   uint32_t red[4][NWV][2];           // per plane and wave: DD aggregate (A, B)
+  uint32_t vd[NWV];                  // each wave's header verdict (ANDed after B2)
+  uint32_t vok[NWV];                 // each wave's DD-header verdict (ANDed after B3)
   uint64_t clk[8];                   // diagnostics: phase clocks (TDBG_PROF)
 };
 
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) v4u g_u4;
+using sc::batch_get;
+using sc::batch_load;
+using sc::Batch;
+using sc::Desc;
+using sc::g_u4;
+using sc::lane_;
+using sc::lds_barrier;
+using sc::v4u;
+using sc::wave_;
 
-__device__ __forceinline__ uint32_t lane_() {
-  uint32_t l = threadIdx.x & 63;
-  asm volatile("" : "+v"(l));
-  return l;
-}
-__device__ __forceinline__ uint32_t wave_() {
-  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-}
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -98,51 +100,8 @@ __device__ __forceinline__ uint32_t c8(const Lds& L, uint32_t o) {
 }
 
 // ---------------------------------------------------------------------------
-// tile descriptors and the LDS-DMA of a tile image
+// the LDS-DMA of a tile image
 // ---------------------------------------------------------------------------
-struct Desc {
-  uint64_t t, fs, os;
-  const uint8_t* in;
-  uint8_t* out;
-};
-
-// Descriptors of the workgroup's tiles, 64 at a time: lane i holds those of
-// its (base + i)-th tile, loaded once (one HBM latency per 64 tiles instead
-// of one per tile) and read back with v_readlane at a uniform index.  The
-// streaming kernel always runs over all tiles (no tile list).
-struct Batch {
-  uint32_t fs, os;  // saturated at 2^32 - 1 (such a tile neither fits nor has 65,536 bytes)
-  uint64_t in, out;
-};
-__device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl) {
-  const uint64_t j = blockIdx.x + (base + (threadIdx.x & 63)) * (uint64_t)gridDim.x;
-  Batch b{0, 0, 0, 0};
-  if (j < ntl) {
-    const uint64_t fs = kp.in_size[j], os = kp.out_size[j];
-    b.fs = fs < 0xffffffffull ? (uint32_t)fs : 0xffffffffu;
-    b.os = os < 0xffffffffull ? (uint32_t)os : 0xffffffffu;
-    b.in = (uint64_t)kp.in[j];
-    b.out = (uint64_t)kp.out[j];
-  }
-  return b;
-}
-// (the builtin returns int: each half goes through uint32_t, or the low half
-// of a pointer would be sign-extended over the high one)
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t k) {
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), k);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, k);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ Desc batch_get(const Batch& b, uint32_t k, uint64_t t) {
-  Desc d;
-  d.t = t;
-  d.fs = (uint32_t)__builtin_amdgcn_readlane(b.fs, k);
-  d.os = (uint32_t)__builtin_amdgcn_readlane(b.os, k);
-  d.in = (const uint8_t*)rl64(b.in, k);
-  d.out = (uint8_t*)rl64(b.out, k);
-  return d;
-}
-
 // the image [in, in + fs) fits the staging window (16-B aligned units)
 __device__ __forceinline__ bool fits(const Desc& d) {
   if (d.fs < 20 || d.fs > CCAP) return false;
@@ -151,37 +110,15 @@ __device__ __forceinline__ bool fits(const Desc& d) {
 }
 
 // LDS-DMA of the image's 16-B units into C: wave w's instruction r moves
-// units [64 (4r + w), +64), lane-linear in LDS.  Inline asm, not the
-// builtin: the compiler would otherwise wait for the DMA (vmcnt(0), which on
-// gfx950 also drains every store before it) at the next LDS read of any
-// address; here the kernel waits for it explicitly, one tile later (wait_dma).
+// units [64 (4r + w), +64), lane-linear in LDS.
 __device__ __forceinline__ void dma(Lds& L, const Desc& d) {
   const uint64_t a0 = (uint64_t)d.in & ~15ull, a1 = ((uint64_t)d.in + d.fs + 15) & ~15ull;
   const uint32_t n16 = (uint32_t)((a1 - a0) >> 4);
   const uint32_t w = wave_(), l = lane_();
   for (uint32_t r = 0; r * NT < n16; r++) {
     const uint32_t ub = r * NT + 64 * w;  // wave-uniform first unit
-    if (ub + l < n16) {
-      const uint64_t src = a0 + 16ull * (ub + l);
-      const uint32_t dst = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)L.C + 16 * ub);
-      uint32_t keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\t"
-          "s_mov_b32 m0, %2\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %1, off\n\t"
-          "s_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
-          : "memory");
-    }
+    if (ub + l < n16) sc::dma16(a0 + 16ull * (ub + l), sc::lds_addr(L.C) + 16 * ub);
   }
-}
-
-// Workgroup barrier for LDS only: no vmcnt drain (outstanding stores and the
-// next tile's DMA stay in flight); "memory" keeps LDS accesses on their side.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -445,7 +382,12 @@ __device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, ui
   b0 = __builtin_amdgcn_readfirstlane(b0);
   if ((mask >> l) & 1) {
     const uint32_t k = b0 + (uint32_t)__builtin_popcountll(mask & ((1ull << l) - 1));
-    if (k < kp.sq_cap) kp.sq[1 + k] = (uint32_t)(blockIdx.x + (uint64_t)(base + l) * gridDim.x);
+    const uint32_t t = (uint32_t)(blockIdx.x + (uint64_t)(base + l) * gridDim.x);
+    // (k < sq_cap always holds -- a tile is queued at most once per launch and
+    // sq_cap = ntiles -- but a tile that would not fit must not be lost: it
+    // gets a status instead of silently keeping whatever its status held)
+    if (k < kp.sq_cap) kp.sq[1 + k] = t;
+    else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
   }
 }
 
@@ -492,7 +434,9 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     if (cur_dma) {
     // B1: this tile's DMA has landed (vmcnt counts in issue order: the last
     // iteration's 16 output stores, issued after the DMA, may stay in flight)
-    if (stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    // (the STM == 3 timing ablation issues its stores under a branch almost
+    // never taken, so it waits for everything)
+    if (stored && STM != 3) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     pc.mark(8);
@@ -566,11 +510,26 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       }
     }
     pc.mark(9);
-    // ok is workgroup-uniform: every wave computed it from the same bytes
+    // Barrier reachability is uniform by construction: every workgroup
+    // barrier below depends only on cur_dma (a function of readlane'd
+    // descriptors); the data-dependent verdicts are published through LDS
+    // and read back after a barrier.  Every wave computed `ok` from the same
+    // bytes, so they agree anyway; every wave takes the AND of all of them.
+    if (l == 0) L.vd[w] = ok ? 1u : 0u;
+    lds_barrier();  // B2: window table + header verdicts
+    {
+      uint32_t all = 1;
+#pragma unroll
+      for (int v = 0; v < NWV; v++) all &= L.vd[v];
+      ok = ok && all != 0;
+    }
+    if (!ok) {
+      wsh = 0;
+      nwin = 1;
+    }
     uint32_t cb = 0, x0 = 0, x1 = 0;
     Win W{wsh, nwin - 1, dst & 3};
     if (ok) {
-      lds_barrier();  // B2: window table
       // DD headers: BWR output bytes [0, 34) = c0 (the byteshuffle md) and c1's
       // header (dd_compressor.cc:314-345); lanes 0..3 decode units 0..3
       const v4u h = bwr_unit<SGN>(L, W, l < 4 ? l : 3);
@@ -605,9 +564,18 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
         default: break;
       }
     }
-    lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals are in red
+    if (l == 0) L.vok[w] = ok ? 1u : 0u;
+    lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals and verdicts are in LDS
+    {
+      uint32_t all = 1;
+#pragma unroll
+      for (int v = 0; v < NWV; v++) all &= L.vok[v];
+      ok = ok && all != 0;
+    }
     }  // cur_dma
-    if (!ok) dmask |= 1ull << (it % 64);
+    // tiles bigger than CCAP belong to the raw-DoubleDelta kernel, which runs
+    // next on every tile and queues the ones it does not take itself
+    if (!ok && cur.fs <= CCAP) dmask |= 1ull << (it % 64);
     if ((it + 1) % 64 == 0 || jn >= ntl) {
       if (dmask && w == 0) queue_batch(kp, dmask, it - it % 64);
       dmask = 0;
@@ -707,16 +675,20 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
 
 // Persistent grid: one workgroup per CU for every TDBG_STREAM_OCC waves per
 // SIMD the registers allow (LDS would hold four).
-extern "C" uint32_t tdbg_stream_grid(int cus) { return (uint32_t)cus * TDBG_STREAM_OCC; }
+extern "C" uint32_t tdbg_stream_grid(int cus) {
+  static const int g = getenv("TDBG_STREAM_GRID") ? atoi(getenv("TDBG_STREAM_GRID")) : 0;  // experiments
+  return g > 0 ? (uint32_t)g : (uint32_t)cus * TDBG_STREAM_OCC;
+}
 
 // Launch: sgn = the BWR stage's integer type is signed.
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
   using namespace tdbg::stream;
-  // experiment switch: 0 plain stores (default), 1 nontemporal stores, 3 no stores (timing)
-  static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 0;
-  auto k = sgn ? (stm == 1 ? unfilter_stream_kernel<true, 1>
-                  : stm == 3 ? unfilter_stream_kernel<true, 3> : unfilter_stream_kernel<true, 0>)
-               : (stm == 1 ? unfilter_stream_kernel<false, 1> : unfilter_stream_kernel<false, 0>);
+  // store mode: 1 nontemporal (default: 5 % faster than plain stores on C5
+  // active, profiles/r03_*), 0 plain, 3 no stores (timing ablation only)
+  static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 1;
+  auto k = sgn ? (stm == 0 ? unfilter_stream_kernel<true, 0>
+                  : stm == 3 ? unfilter_stream_kernel<true, 3> : unfilter_stream_kernel<true, 1>)
+               : (stm == 0 ? unfilter_stream_kernel<false, 0> : unfilter_stream_kernel<false, 1>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
   return hipGetLastError();
 }

@@ -6,6 +6,7 @@ done by libtiledb_amd.so.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 from typing import Optional, Sequence
 
@@ -13,6 +14,11 @@ import numpy as np
 
 from . import _native
 from ._native import lib
+
+# At interpreter exit the HIP runtime may already be torn down: handles still
+# alive then are left to the OS (no destroy calls, no errors during shutdown).
+_SHUTDOWN: list = []
+atexit.register(lambda: _SHUTDOWN.append(True))
 
 TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
 HOST_CONTIGUOUS_INPUT = 0x2   # TDBG_HOST_CONTIGUOUS_INPUT
@@ -60,10 +66,10 @@ class DevicePipeline:
                "tdbg_pipeline_filter")
         return int(t.value), int(d.value)
 
-    def __del__(self):
+    def __del__(self, _destroy=lib.tdbg_pipeline_destroy, _down=_SHUTDOWN):
         h = getattr(self, "h", None)
-        if h:
-            lib.tdbg_pipeline_destroy(h)
+        if h and not _down:
+            _destroy(h)
             self.h = None
 
 
@@ -210,10 +216,10 @@ class Context:
         self.h = h
         self.device = device
 
-    def __del__(self):
+    def __del__(self, _destroy=lib.tdbg_context_destroy, _down=_SHUTDOWN):
         h = getattr(self, "h", None)
-        if h:
-            lib.tdbg_context_destroy(h)
+        if h and not _down:
+            _destroy(h)
             self.h = None
 
     @staticmethod
@@ -282,6 +288,12 @@ class Context:
         """Fused tiles the streaming C5 kernel took, cumulative (synchronizes)."""
         n = ctypes.c_uint64()
         _check(lib.tdbg_context_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_stats")
+        return int(n.value)
+
+    def stream_raw_tiles(self):
+        """Of those, the tiles the raw-DoubleDelta streaming kernel took, cumulative."""
+        n = ctypes.c_uint64()
+        _check(lib.tdbg_context_stream_raw_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_raw_stats")
         return int(n.value)
 
     def stats(self):
