@@ -84,10 +84,21 @@ def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, devic
     idx = np.arange(ntiles) % nunique
     sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
     offs = engine.pack_offsets(sizes, align)
-    packed = np.zeros(int(offs[-1] + sizes[-1]), dtype=np.uint8)
+    total = int(offs[-1] + sizes[-1])
     pool_np = [np.frombuffer(p, dtype=np.uint8) for p in pool]
-    for k, (i, o) in enumerate(zip(idx, offs)):
-        packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
+    if ntiles > nunique:
+        # tile k sits at (k // nunique) * period + offs[k % nunique]: pack one
+        # period of the unique tiles, then repeat it
+        period = int(offs[nunique])
+        blk = np.zeros(period, dtype=np.uint8)
+        for i in range(nunique):
+            blk[int(offs[i]):int(offs[i]) + pool_np[i].size] = pool_np[i]
+        packed = np.tile(blk, -(-total // period))[:total]
+        assert int(offs[-1]) == (ntiles - 1) // nunique * period + int(offs[(ntiles - 1) % nunique])
+    else:
+        packed = np.zeros(total, dtype=np.uint8)
+        for i, o in zip(idx, offs):
+            packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
     out_sizes = [vals[i].nbytes for i in idx]
     batch = engine.TileBatch.from_packed(packed, offs, sizes, out_sizes, device=device)
     return batch, pool, vals, idx, packed, offs, sizes
@@ -260,6 +271,179 @@ def load_traffic(cfg: str, variant: str):
         return None
 
 
+def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, dist, world, rank,
+               forward=False, e2e_leg=False, align=1):
+    """Build and time one config's variants; returns (DevicePipeline, {variant: result})."""
+    import torch
+    ser, dt, cs, _, _ = W.config(cfgname)
+    dp = engine.DevicePipeline(ser, 23, int(dt), cs)
+    # timing-only ablations (outputs unchecked): TDBG_DEBUG_STOP (fused
+    # kernel stages) or TDBG_BENCH_NOVERIFY (e.g. TDBG_RAW_ABL, TDBG_STREAM_STORE=3)
+    ablation = bool(os.environ.get("TDBG_DEBUG_STOP") or os.environ.get("TDBG_BENCH_NOVERIFY"))
+    res = {}
+    for vi, var in enumerate(variants):
+        batch, pool, vals, idx, packed, offs, sizes = build_batch(
+            engine, cfgname, var, ntiles, args.unique, torch.cuda.current_device(), seed=5 + 1000 * rank + vi,
+            align=align, ctx=ctx, dp=dp)
+        st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
+        if st.any():
+            raise SystemExit(f"{cfgname} {var}: first pass status nonzero: {np.unique(st)}")
+        if not ablation:
+            verify(batch, vals, idx)
+        elapsed, kern_ms, launch_ms, fused, fallback, streamed = time_device(
+            engine, ctx, dp, batch, steps, warmup, dist, world)
+        if not ablation:
+            verify(batch, vals, idx)
+        unf = float(sum(vals[i].nbytes for i in idx))
+        b_alg = float(sizes.sum()) + unf
+        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
+                        out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback, streamed=streamed,
+                        packed=packed, offs=offs, sizes=sizes, steps=steps, ntiles=ntiles)
+        if forward and vi == 0 and not ablation and cfgname != "fscale":  # (lossy: values differ)
+            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, steps, warmup, dist)
+        if e2e_leg:
+            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args, dist, world)
+        del batch
+        torch.cuda.empty_cache()
+    return dp, res
+
+
+def gibps(r, world):
+    return r["unf"] * world / (r["elapsed"] / r["steps"]) / 2**30
+
+
+def frac(r):
+    return r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+
+
+def kernel_name(cfgname, r):
+    if cfgname in ("c5", "c5big") and r["streamed"]:
+        return ("unfilter_stream_kernel + unfilter_stream_raw_kernel + unfilter_fused_kernel (queue of "
+                "declined tiles)")
+    return "unfilter_fused_kernel"
+
+
+def roofline(cfgname, var, r):
+    achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
+    traffic = load_traffic(cfgname, var)
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_source": f"{TRAFFIC_FILE} (committed rocprofv3 --pmc passes of this workload)" if traffic else None,
+        # kernel_ms: the launch's unfilter kernels on its stream, HIP events
+        "kernel": kernel_name(cfgname, r),
+        "kernel_ms": round(r["kern_ms"], 4),
+        "launch_ms": round(r["launch_ms"], 4),
+        "algorithmic_bytes_per_launch": int(r["b_alg"]),
+    }
+
+
+def variant_line(cfgname, var, r, world):
+    return {"GiBps": round(gibps(r, world), 2), "roofline_frac": round(frac(r), 4),
+            "kernel_ms": round(r["kern_ms"], 4), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
+            "fallback_tiles_timed": r["fallback"], "stream_tiles_timed": r["streamed"],
+            "algorithmic_bytes_per_launch": int(r["b_alg"]),
+            "traffic": load_traffic(cfgname, var)}
+
+
+def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048):
+    cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
+                                ntiles_sample, threads, seconds)
+    return {
+        "value": round(cpu, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{ntl} {cfgname.upper()} '{var}' tiles ({min(ntiles_sample, r['offs'].size)}-tile sample, "
+                  f"repeated) in {el:.2f}s on {threads} threads of '{cpu_model()}' ({os.cpu_count()} CPUs "
+                  "visible; 16 threads = one GPU's share of the box), tdbg_unfilter_tiles_cpu (the C-ABI's "
+                  "C++ CPU entry, the reference's tile x chunk-range split)",
+    }
+
+
+# the other BASELINE configs timed in the default (N = 1) run, per-GPU sizes
+OTHER_CONFIGS = ("c1", "c2", "c2i", "c3a", "c3b", "c4")
+
+
+def headline_line(args, W, variants, res, world):
+    """The JSON line of the bench's config: `value` is the slowest variant
+    (SURVEY 8(d) defines C5's 'ramp' and 'rand'; 'active' makes all three
+    stages work), so the headline is a floor over the data variants."""
+    cfg = CONFIGS[args.config]
+    head = min(variants, key=lambda v: gibps(res[v], world))
+    r = res[head]
+    line = {
+        "metric": "GiB/s unfiltered tile bytes (device-resident), 64 KiB chunks, 3-stage pipeline",
+        "value": round(gibps(r, world), 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": r["steps"],
+        "warmup": args.warmup,
+        "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": cfg["dtype"],
+        "data": f"synthetic {args.config.upper()} tiles, variants {','.join(variants)} ({args.unique} unique each, "
+                "replicated), " + ("device-encoded (tdbg_filter_tiles)" if W.config(args.config)[4] is None
+                                   else "numpy-encoded (workloads.py)"),
+        "config": {
+            "workload": cfg["workload"],
+            "tiles_per_gpu": r["ntiles"],
+            "variant": head if len(variants) == 1 else f"min over {','.join(variants)} = '{head}'",
+            "tile_alignment": args.align,
+            "parallelism": f"tile-shard x{world} (no collectives)",
+            "filtered_bytes_per_gpu": int(r["sizes"].sum()),
+            "fused_tiles_timed": r["fused"],
+            "fallback_tiles_timed": r["fallback"],
+            "stream_tiles_timed": r["streamed"],
+        },
+        "roofline": roofline(args.config, head, r),
+    }
+    line["config"]["variants"] = {v: variant_line(args.config, v, res[v], world) for v in variants}
+    line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v], world) for v in variants), 2)
+    line["config"]["min_over_variants_roofline_frac"] = round(min(frac(res[v]) for v in variants), 4)
+    fv = variants[0]
+    if "fwd" in res[fv]:
+        el, fk, fb_alg, fin = res[fv]["fwd"]
+        line["forward"] = {
+            "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
+            "variant": fv,
+            "value": round(fin * world / (el / r["steps"]) / 2**30, 2),
+            "unit": "GiB/s",
+            "ms_per_step": round(el / r["steps"] * 1e3, 4),
+            "kernel": "filter_tiles_kernel",
+            "kernel_ms": round(fk, 4),
+            "algorithmic_bytes_per_launch": int(fb_alg),
+            "roofline_frac": round(fb_alg / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+    if all("e2e" in res[v] for v in variants):
+        line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
+        line["config"]["e2e_note"] = ("pinned host tiles -> H2D -> unfilter -> D2H into a pinned result buffer, "
+                                      "TDBG_HOST_CONTIGUOUS_INPUT|OUTPUT (one FilteredData-style block each way), "
+                                      f"{args.e2e_batch_mb} MiB batches; PCIe-bound, never `value`")
+    return line
+
+
+def init_dist(dist_mod, torch, env, local: int) -> str:
+    """One process per GPU: RCCL ('nccl') bound to the rank's own device
+    (init_process_group(device_id=cuda:local)), or the gloo rehearsal
+    (TDBG_DIST_BACKEND=gloo) with ranks sharing the box's GPUs round-robin.
+    Returns the device the max-over-ranks reduction runs on."""
+    be, dev = dist_backend(env, local, torch.cuda.device_count())
+    if dev is None:
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group(be, device_id=torch.device("cuda", local))
+        return "cuda"
+    torch.cuda.set_device(dev)
+    dist_mod.init_process_group(be)
+    return "cpu"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,15 +460,22 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds-other", type=float, default=2.0,
+                    help="CPU baseline sample time per other config")
     ap.add_argument("--e2e", action="store_true", default=True,
                     help="also time host-resident end-to-end (default on; every rank, "
                          "total over ranks / max-over-ranks time)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false")
     ap.add_argument("--forward", action="store_true", default=True,
-                    help="also time the forward (filter) direction on the headline variant (default on)")
+                    help="also time the forward (filter) direction on the first variant (default on)")
     ap.add_argument("--no-forward", dest="forward", action="store_false")
     ap.add_argument("--e2e-batch-mb", type=int, default=64,
                     help="host E2E staging batch (MiB per side; 2 batches in flight)")
+    ap.add_argument("--others", action="store_true", default=True,
+                    help="N = 1 default C5 run: also time every other BASELINE config (config.other_configs) "
+                         "and C5 at 100k tiles on the one GPU")
+    ap.add_argument("--no-others", dest="others", action="store_false")
+    ap.add_argument("--big-tiles", type=int, default=100000, help="tiles of the single-GPU C5 leg")
     args = ap.parse_args()
 
     import torch
@@ -295,15 +486,7 @@ def main():
     if world > 1:
         import torch.distributed as dist_mod
         global DIST_DEV
-        if os.environ.get("TDBG_DIST_BACKEND", "nccl") == "gloo":
-            # rehearsal: ranks may share a GPU (the box has one); same barrier
-            # and max-over-ranks timing, reduced on the CPU
-            torch.cuda.set_device(local % torch.cuda.device_count())
-            dist_mod.init_process_group("gloo")
-            DIST_DEV = "cpu"
-        else:
-            torch.cuda.set_device(local)
-            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        DIST_DEV = init_dist(dist_mod, torch, os.environ, local)
         dist = dist_mod
     else:
         torch.cuda.set_device(0)
@@ -312,135 +495,64 @@ def main():
 
     cfg = CONFIGS[args.config]
     ntiles = args.tiles_per_gpu or cfg["tiles_per_gpu"]
-    ser, dt, cs, _, _ = W.config(args.config)
-    dp = engine.DevicePipeline(ser, 23, int(dt), cs)
     ctx = engine.Context(torch.cuda.current_device())  # this rank's GPU (set above)
     variants = [v for v in (args.variants or cfg["variants"]).split(",") if v]
-    res = {}
-    for vi, var in enumerate(variants):
-        batch, pool, vals, idx, packed, offs, sizes = build_batch(
-            engine, args.config, var, ntiles, args.unique, torch.cuda.current_device(), seed=5 + 1000 * rank + vi,
-            align=args.align, ctx=ctx, dp=dp)
-        # timing-only ablations (outputs unchecked): TDBG_DEBUG_STOP (fused
-        # kernel stages) or TDBG_BENCH_NOVERIFY (e.g. TDBG_RAW_ABL, TDBG_STREAM_STORE=3)
-        ablation = bool(os.environ.get("TDBG_DEBUG_STOP") or os.environ.get("TDBG_BENCH_NOVERIFY"))
-        st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
-        if st.any():
-            raise SystemExit(f"{var}: first pass status nonzero: {np.unique(st)}")
-        if not ablation:
-            verify(batch, vals, idx)
-        elapsed, kern_ms, launch_ms, fused, fallback, streamed = time_device(
-            engine, ctx, dp, batch, args.steps, args.warmup, dist, world)
-        if not ablation:
-            verify(batch, vals, idx)
-        unf = float(sum(vals[i].nbytes for i in idx))
-        b_alg = float(sizes.sum()) + unf
-        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
-                        out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback, streamed=streamed,
-                        packed=packed, offs=offs, sizes=sizes)
-        if args.forward and vi == 0 and not ablation and args.config != "fscale":  # (lossy: values differ)
-            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, args.steps, args.warmup, dist)
-        if args.e2e:
-            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args,
-                                  dist, world)
-        del batch
-        torch.cuda.empty_cache()
+    dp, res = run_config(engine, ctx, W, args, args.config, variants, ntiles, args.steps, args.warmup, dist,
+                         world, rank, forward=args.forward, e2e_leg=args.e2e, align=args.align)
 
-    def gibps(r):
-        return r["unf"] * world / (r["elapsed"] / args.steps) / 2**30
-
-    def frac(r):
-        return r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
-
-    head = variants[0]
+    line = headline_line(args, W, variants, res, world)
+    head = min(variants, key=lambda v: gibps(res[v], world))
     r = res[head]
-    ms_per_step = r["elapsed"] / args.steps * 1e3
-    value = gibps(r)
-    achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
-    traffic = load_traffic(args.config, head)
-    line = {
-        "metric": "GiB/s unfiltered tile bytes (device-resident), 64 KiB chunks, 3-stage pipeline",
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": cfg["dtype"],
-        "data": f"synthetic {args.config.upper()} '{head}' tiles ({args.unique} unique, replicated), "
-                + ("device-encoded (tdbg_filter_tiles)" if W.config(args.config)[4] is None
-                   else "numpy-encoded (workloads.py)"),
-        "config": {
-            "workload": cfg["workload"],
-            "tiles_per_gpu": ntiles,
-            "variant": head,
-            "tile_alignment": args.align,
-            "parallelism": f"tile-shard x{world} (no collectives)",
-            "filtered_bytes_per_gpu": int(r["sizes"].sum()),
-            "fused_tiles_timed": r["fused"],
-            "fallback_tiles_timed": r["fallback"],
-            "stream_tiles_timed": r["streamed"],
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_source": f"{TRAFFIC_FILE} (committed rocprofv3 --pmc passes of this workload)"
-                              if traffic else None,
-            # kernel_ms: the launch's unfilter kernels on its stream (HIP events):
-            # for C5 the streaming kernel, then the fused kernel on its queue
-            "kernel": ("unfilter_stream_kernel + unfilter_fused_kernel (stream queue)" if r["streamed"]
-                       else "unfilter_fused_kernel"),
-            "kernel_ms": round(r["kern_ms"], 4),
-            "launch_ms": round(r["launch_ms"], 4),
-            "algorithmic_bytes_per_launch": int(r["b_alg"]),
-        },
-    }
-    if len(variants) > 1:
-        line["config"]["variants"] = {
-            v: {"GiBps": round(gibps(res[v]), 2), "roofline_frac": round(frac(res[v]), 4),
-                "kernel_ms": round(res[v]["kern_ms"], 4), "fallback_tiles_timed": res[v]["fallback"],
-                "stream_tiles_timed": res[v]["streamed"],
-                "algorithmic_bytes_per_launch": int(res[v]["b_alg"])}
-            for v in variants}
-        line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v]) for v in variants), 2)
-    if "fwd" in r:
-        el, fk, fb_alg, fin = r["fwd"]
-        line["forward"] = {
-            "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
-            "value": round(fin * world / (el / args.steps) / 2**30, 2),
-            "unit": "GiB/s",
-            "ms_per_step": round(el / args.steps * 1e3, 4),
-            "kernel": "filter_tiles_kernel",
-            "kernel_ms": round(fk, 4),
-            "algorithmic_bytes_per_launch": int(fb_alg),
-            "roofline_frac": round(fb_alg / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        }
-    if args.e2e:
-        line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
-                                    2048, threads, args.cpu_seconds)
-        line["cpu_baseline"] = {
-            "value": round(cpu, 3),
-            "unit": "GiB/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": f"{ntl} {args.config.upper()} '{head}' tiles (2048-tile sample, repeated) in {el:.2f}s "
-                      f"on {threads} threads of '{cpu_model()}' ({os.cpu_count()} CPUs visible), "
-                      "tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry)",
-        }
+    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    if world == 1 and args.others and args.config == "c5" and not args.tiles_per_gpu:
+        # every other BASELINE config at its per-GPU size, and C5 at 100k tiles
+        others = {}
+        for c in OTHER_CONFIGS:
+            cc = CONFIGS[c]
+            cvars = [v for v in cc["variants"].split(",") if v]
+            cdp, cres = run_config(engine, ctx, W, args, c, cvars, cc["tiles_per_gpu"], args.steps, args.warmup,
+                                   dist, world, rank)
+            ch = min(cvars, key=lambda v: gibps(cres[v], world))
+            o = {"workload": cc["workload"], "tiles_per_gpu": cc["tiles_per_gpu"], "dtype": cc["dtype"],
+                 "value_GiBps": round(gibps(cres[ch], world), 2), "variant": ch,
+                 "roofline": roofline(c, ch, cres[ch]),
+                 "variants": {v: variant_line(c, v, cres[v], world) for v in cvars}}
+            if not args.no_cpu_baseline:
+                o["cpu_baseline"] = cpu_line(engine, cdp, cres[ch], c, ch, threads, args.cpu_seconds_other)
+            if c == "c1":
+                o["note"] = ("BASELINE names C1 a CPU-path config: cpu_baseline is that path (the C++ CPU entry); "
+                             "the GPU line is the same tiles on the device")
+            others[c] = o
+            for v in cres:  # free the host copies
+                cres[v].pop("packed", None)
+        line["config"]["other_configs"] = others
+        # C5 at its full BASELINE size (100k tiles) on this one GPU
+        big = {}
+        _, bres = run_config(engine, ctx, W, args, "c5", variants, args.big_tiles, max(3, args.steps // 4),
+                             2, dist, world, rank)
+        for v in variants:
+            big[v] = variant_line("c5big", v, bres[v], world)
+            bres[v].pop("packed", None)
+        line["config"]["c5_100k_single_gpu"] = {
+            "tiles": args.big_tiles, "steps": max(3, args.steps // 4), "variants": big,
+            "min_over_variants_GiBps": round(min(x["GiBps"] for x in big.values()), 2),
+            "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in big.values()), 4)}
+    if rank == 0 and not args.no_cpu_baseline:
+        # after every timed region, at any N (rank 0 only)
+        line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dist_backend(env, local: int, ndev: int):
+    """(backend, device for gloo or None): RCCL ('nccl') with each rank on
+    its own GPU, or the gloo rehearsal (TDBG_DIST_BACKEND=gloo) where ranks
+    may share the box's GPUs round-robin."""
+    if env.get("TDBG_DIST_BACKEND", "nccl") == "gloo":
+        return "gloo", local % max(1, ndev)
+    return "nccl", None
 
 
 def e2e(engine, ctx, dp, packed, offs, sizes, out_bytes, args, dist=None, world=1):

@@ -111,8 +111,10 @@ enum tdbg_status {
   TDBG_E_DESCRIPTOR = 15,   /* malformed serialized pipeline                    */
   TDBG_E_DELTA_TYPE = 16,   /* Delta float: "Decompression is not yet supported for
                                float datatypes." delta_compressor.cc:210-213   */
-  TDBG_E_INTERNAL = 17      /* internal engine error (a device work queue overflowed):
+  TDBG_E_INTERNAL = 17,     /* internal engine error (a device work queue overflowed):
                                the tile was not unfiltered; never expected   */
+  TDBG_E_IO = 18            /* tdbg_read_unfilter_tiles: a block read failed
+                               (VFS::read_exactly: short read or I/O error)  */
 };
 
 /* unfilter flags */
@@ -356,6 +358,92 @@ int tdbg_device_free(void* p);
 int tdbg_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
 int tdbg_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
 int tdbg_device_count(int* n);
+
+/* ======================================================================
+ * The steps either side of the path
+ * ====================================================================== */
+
+/* Device index of a context. */
+int tdbg_context_device(const tdbg_context* ctx);
+
+/* Pinned host memory on the device's NUMA node (the calling thread is bound
+ * to the device's local CPUs while the pages are allocated and first
+ * touched), for staging and result buffers the H2D / D2H DMA reads/writes. */
+int tdbg_host_alloc_local(int device, uint64_t bytes, void** out);
+int tdbg_host_free(void* p);
+
+/* FilteredData block rule (filtered_data.h:503-540): tiles in result-tile
+ * order, tile i at file_offset[i] (size[i]) of file file_idx[i]; a tile
+ * extends the current block when it is in the same file, the block stays <=
+ * max_batch_size, and the block is <= min_batch_size or the gap to the tile
+ * is <= min_batch_gap.  block_first_tile (ntiles + 1 entries) receives the
+ * first tile of each block and, after the last block, ntiles. */
+int tdbg_filtered_data_blocks(uint64_t ntiles, const uint32_t* file_idx, const uint64_t* file_offset,
+                              const uint64_t* size, uint64_t min_batch_size, uint64_t max_batch_size,
+                              uint64_t min_batch_gap, uint64_t* block_first_tile, uint64_t* nblocks);
+
+typedef struct tdbg_read_config {
+  uint64_t min_batch_size;  /* 0: vfs.min_batch_size default, 20 MiB (config.cc:165) */
+  uint64_t max_batch_size;  /* 0: vfs.max_batch_size default, 100 MiB (config.cc:163) */
+  uint64_t min_batch_gap;   /* 0: vfs.min_batch_gap default, 500 KB (config.cc:164),
+                               unless TDBG_READ_ZERO_GAP */
+  uint32_t io_threads;      /* 0: 4 (the reference's IO thread pool role) */
+  uint32_t slots;           /* pinned block slots, >= 2 (0: 3) */
+  uint32_t flags;
+} tdbg_read_config;
+#define TDBG_READ_ZERO_GAP 0x1u /* min_batch_gap = 0 is meant literally */
+
+/* Read + unfilter: ReaderBase::read_tiles (reader_base.cc:689-789) ->
+ * FilteredData blocks read with pread (VFS::read_exactly,
+ * filtered_data.h:397-398) by IO threads into NUMA-local pinned slots, each
+ * landed block unfiltered by tdbg_unfilter_tiles_host (H2D -> kernels ->
+ * D2H into out[i]) while later blocks are read.  fds[f] is an open file
+ * descriptor of fragment file f.  Tiles of a failed block read get
+ * TDBG_E_IO.  For full speed the out buffers should be pinned
+ * (tdbg_host_alloc_local). */
+int tdbg_read_unfilter_tiles(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t ntiles, const int* fds,
+                             uint32_t nfiles, const uint32_t* file_idx, const uint64_t* file_offset,
+                             const uint64_t* persisted_size, uint8_t* const* out, const uint64_t* out_size,
+                             uint32_t flags, const tdbg_read_config* cfg, int32_t* host_status);
+
+/* Dense cell-slab copy (DenseReader::copy_fixed_tiles,
+ * dense_reader.cc:1555-1750) for one fragment covering the subarray: the
+ * cells of subarray [sub_lo, sub_hi] (one inclusive range per dimension) are
+ * copied from the unfiltered tiles -- tile t covers [tile_start[t*dim_num + d],
+ * + tile_extent[d]) in cell order cell_order -- into a result buffer in the
+ * query layout (row-major: last dimension fastest).  Same order: slab
+ * memcpy; different: cell by cell, as the reference. */
+#define TDBG_DENSE_MAX_DIMS 4
+typedef struct tdbg_dense_copy_config {
+  uint32_t dim_num;     /* 1..TDBG_DENSE_MAX_DIMS */
+  uint32_t cell_size;   /* bytes per cell (fixed-size attribute) */
+  uint32_t cell_order;  /* tile cell order: 0 row-major, 1 col-major */
+  uint32_t layout;      /* result layout: 0 row-major, 1 col-major */
+  int64_t tile_extent[TDBG_DENSE_MAX_DIMS];
+  int64_t sub_lo[TDBG_DENSE_MAX_DIMS];
+  int64_t sub_hi[TDBG_DENSE_MAX_DIMS];
+} tdbg_dense_copy_config;
+
+/* Bytes of the result buffer of a dense copy: prod(sub_hi - sub_lo + 1) * cell_size
+ * (0 for an invalid config). */
+uint64_t tdbg_dense_result_bytes(const tdbg_dense_copy_config* cfg);
+
+/* Device-resident: unfiltered device tiles d_tiles[t] (tile starts in
+ * d_tile_start, device) -> device result buffer; tiles whose d_status is not
+ * TDBG_OK (if given) are skipped. */
+int tdbg_dense_copy_async(tdbg_context* ctx, const tdbg_dense_copy_config* cfg, uint64_t ntiles,
+                          const int64_t* d_tile_start, const uint8_t* const* d_tiles, const int32_t* d_status,
+                          uint8_t* d_result, tdbg_stream stream);
+
+/* The dense read of a field with copy_attribute fused into the transfer:
+ * filtered host tiles -> H2D -> unfilter -> cell-slab copy into a device
+ * result buffer -> one D2H of the result (result_size >=
+ * tdbg_dense_result_bytes), so PCIe carries the filtered tiles in and only
+ * the subarray's cells out.  tile_start: host, ntiles * dim_num. */
+int tdbg_dense_read_host(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t ntiles, const uint8_t* const* in,
+                         const uint64_t* in_size, const int64_t* tile_start, const tdbg_dense_copy_config* cfg,
+                         uint8_t* result, uint64_t result_size, uint32_t flags, int32_t* host_status,
+                         uint64_t batch_bytes);
 
 #ifdef __cplusplus
 }

@@ -205,3 +205,65 @@ def byteshuffle(data, ts: int, inverse: bool = False) -> bytes:
 
 def compute_chunk_size(tile_size: int, cell_size: int, max_chunk: int = 0) -> int:
     return lib().oracle_compute_chunk_size(tile_size, cell_size, max_chunk)
+
+
+# ---------------------------------------------------------------------------
+# the steps either side of the path, restated in numpy
+# ---------------------------------------------------------------------------
+def filtered_data_blocks(file_idx, file_offset, size, min_batch_size: int = 20971520,
+                         max_batch_size: int = 104857600, min_batch_gap: int = 512000):
+    """FilteredData::make_new_block_if_required (filtered_data.h:503-540),
+    one TileType: tiles in result-tile order; a tile extends the current block
+    iff same fragment, new_size <= max_batch_size and (new_size <=
+    min_batch_size or gap <= min_batch_gap), with the reference's unsigned
+    64-bit arithmetic for new_size and gap.  Returns the first tile of every
+    block followed by ntiles."""
+    M = (1 << 64) - 1
+    first = []
+    cur = None
+    boff = bsize = 0
+    for i, (f, off, sz) in enumerate(zip(file_idx, file_offset, size)):
+        off, sz = int(off), int(sz)
+        if cur is None:
+            first.append(i)
+            boff, bsize, cur = off, sz, int(f)
+            continue
+        new_size = ((off + sz) - boff) & M
+        gap = (off - (boff + bsize)) & M
+        if cur == int(f) and new_size <= max_batch_size and (new_size <= min_batch_size or gap <= min_batch_gap):
+            bsize = new_size
+        else:
+            first.append(i)
+            boff, bsize, cur = off, sz, int(f)
+    return first + [len(size)]
+
+
+def dense_subarray_cells(tiles, tile_start, tile_extent, cell_size: int, sub_lo, sub_hi,
+                         cell_order: int = 0, layout: int = 0) -> np.ndarray:
+    """DenseReader::copy_fixed_tiles (dense_reader.cc:1555-1750) for one
+    fragment covering the subarray: the subarray's cells, from the tiles
+    (tile t holds the cells [tile_start[t], + tile_extent) in cell order
+    cell_order: 0 row-major, 1 col-major), in result layout `layout`.  Cells
+    are cell_size-byte records."""
+    nd = len(tile_extent)
+    ext = [int(e) for e in tile_extent]
+    lo = [int(x) for x in sub_lo]
+    hi = [int(x) for x in sub_hi]
+    shape = tuple(h - l + 1 for l, h in zip(lo, hi))
+    out = np.zeros(shape + (cell_size,), dtype=np.uint8)
+    for t, raw in enumerate(tiles):
+        s = [int(x) for x in tile_start[t]]
+        a = [max(s[d], lo[d]) for d in range(nd)]
+        b = [min(s[d] + ext[d] - 1, hi[d]) for d in range(nd)]
+        if any(b[d] < a[d] for d in range(nd)):
+            continue
+        cells = np.frombuffer(bytes(raw), dtype=np.uint8).reshape(-1, cell_size)
+        blk = cells.reshape(tuple(ext) + (cell_size,) if cell_order == 0 else tuple(reversed(ext)) + (cell_size,))
+        if cell_order == 1:  # col-major: the first dimension fastest
+            blk = np.transpose(blk, tuple(reversed(range(nd))) + (nd,))
+        src = tuple(slice(a[d] - s[d], b[d] - s[d] + 1) for d in range(nd))
+        dst = tuple(slice(a[d] - lo[d], b[d] - lo[d] + 1) for d in range(nd))
+        out[dst] = blk[src]
+    if layout == 1:
+        out = np.transpose(out, tuple(reversed(range(nd))) + (nd,))
+    return np.ascontiguousarray(out).reshape(-1)

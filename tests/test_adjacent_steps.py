@@ -1,0 +1,222 @@
+"""The steps either side of the path, through the C-ABI.
+
+* FilteredData-style reads (tdbg_filtered_data_blocks / tdbg_read_unfilter_tiles):
+  the block rule against the oracle's restatement of
+  FilteredData::make_new_block_if_required (filtered_data.h:503-540) on the CPU,
+  and on the GPU tiles read from fragment files by IO threads into
+  NUMA-local pinned blocks, unfiltered, bit-exact against the oracle.
+* Dense cell-slab copy fused with the D2H (tdbg_dense_read_host /
+  tdbg_dense_copy_async): the subarray's cells against the oracle's
+  restatement of DenseReader::copy_fixed_tiles (dense_reader.cc:1555-1750)
+  for row/col-major cell orders and layouts, 1-3 dimensions, partial tiles.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import workloads as W
+from tiledb_amd.filter_pipeline import ByteshuffleFilter, Datatype, FilterPipeline
+
+
+# ---------------------------------------------------------------------------
+# CPU: the block rule
+# ---------------------------------------------------------------------------
+def _random_layout(rng, ntiles, nfiles):
+    fi = np.sort(rng.integers(0, nfiles, ntiles)).astype(np.uint32)
+    size = rng.integers(1, 5000, ntiles).astype(np.uint64)
+    off = np.zeros(ntiles, dtype=np.uint64)
+    pos = {}
+    for i in range(ntiles):
+        f = int(fi[i])
+        gap = int(rng.choice([0, 0, 7, 300, 5000, 200000]))
+        off[i] = pos.get(f, 0) + gap
+        pos[f] = int(off[i] + size[i])
+    return fi, off, size
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("params", [(20971520, 104857600, 512000), (3000, 20000, 10), (0, 8000, 0),
+                                    (10**9, 10**9, 10**9), (100, 100, 0)])
+def test_filtered_data_blocks_match_reference_rule(oracle_mod, seed, params):
+    from tiledb_amd import engine
+    rng = np.random.default_rng(seed)
+    fi, off, size = _random_layout(rng, 200, 3)
+    got = engine.filtered_data_blocks(fi, off, size, *params)
+    want = oracle_mod.filtered_data_blocks(fi, off, size, *params)
+    assert got.tolist() == want
+
+
+def test_filtered_data_blocks_edge_cases(oracle_mod):
+    from tiledb_amd import engine
+    assert engine.filtered_data_blocks([], [], []).tolist() == [0]
+    assert engine.filtered_data_blocks([0], [5], [10]).tolist() == [0, 1]
+    # overlapping / out-of-order offsets: the reference's unsigned gap wraps
+    fi, off, size = [0, 0, 0], [100, 50, 400], [10, 10, 10]
+    assert engine.filtered_data_blocks(fi, off, size, 30, 1000, 5).tolist() == \
+        oracle_mod.filtered_data_blocks(fi, off, size, 30, 1000, 5)
+
+
+# ---------------------------------------------------------------------------
+# GPU: read + unfilter from fragment files
+# ---------------------------------------------------------------------------
+def _c5_pipe():
+    return W.c5_pipeline_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_kind", ["default", "small_blocks", "zero_gap"])
+def test_read_unfilter_tiles_from_files(oracle_mod, cfg_kind):
+    import torch
+    assert torch.cuda.is_available()
+    from tiledb_amd import _native, engine
+    rng = np.random.default_rng(41)
+    pools = []
+    for var in ("active", "ramp", "rand"):
+        pools += list(zip(*W.c5_pool(var, 6, seed=42)))
+    # three fragment files; tiles at their offsets with gaps between some
+    nfiles = 3
+    tiles, vals, fidx, foff = [], [], [], []
+    with tempfile.TemporaryDirectory() as tmp:
+        paths = [os.path.join(tmp, f"frag{f}.tdb") for f in range(nfiles)]
+        blobs = [bytearray() for _ in range(nfiles)]
+        order = rng.permutation(len(pools) * 3)
+        for k in order:
+            f = int(k % nfiles)
+            t, v = pools[int(k) % len(pools)]
+            blobs[f] += bytes(int(rng.choice([0, 0, 16, 3000, 700000])))
+            fidx.append(f)
+            foff.append(len(blobs[f]))
+            blobs[f] += t
+            tiles.append(t)
+            vals.append(v)
+        for pth, b in zip(paths, blobs):
+            with open(pth, "wb") as fh:
+                fh.write(bytes(b))
+        # result-tile order: by fragment, then offset
+        srt = sorted(range(len(tiles)), key=lambda i: (fidx[i], foff[i]))
+        tiles = [tiles[i] for i in srt]
+        vals = [vals[i] for i in srt]
+        fidx = np.array([fidx[i] for i in srt], dtype=np.uint32)
+        foff = np.array([foff[i] for i in srt], dtype=np.uint64)
+        size = np.array([len(t) for t in tiles], dtype=np.uint64)
+        fds = [os.open(pth, os.O_RDONLY) for pth in paths]
+        try:
+            ctx = engine.Context(0)
+            dp = engine.DevicePipeline(_c5_pipe(), 23, int(Datatype.INT32), 4)
+            res = engine.HostBuffer(0, len(tiles) * W.TILE_BYTES)
+            out_ptrs = res.ptr + np.arange(len(tiles), dtype=np.uint64) * np.uint64(W.TILE_BYTES)
+            cfg = _native.ReadConfig()
+            if cfg_kind == "small_blocks":
+                cfg.min_batch_size, cfg.max_batch_size, cfg.min_batch_gap = 100000, 300000, 100
+                cfg.io_threads, cfg.slots = 2, 2
+            elif cfg_kind == "zero_gap":
+                cfg.min_batch_size, cfg.flags = 1, 0x1  # TDBG_READ_ZERO_GAP
+            st = ctx.read_unfilter(dp, fds, fidx, foff, size, out_ptrs,
+                                   np.full(len(tiles), W.TILE_BYTES, dtype=np.uint64), cfg=cfg)
+            assert not st.any(), np.unique(st)
+            op = oracle_mod.OraclePipeline(_c5_pipe(), 23, int(Datatype.INT32), 4)
+            for i, t in enumerate(tiles):
+                got = res.array[i * W.TILE_BYTES:(i + 1) * W.TILE_BYTES]
+                rc, ref = op.unfilter_tile(np.frombuffer(t, dtype=np.uint8), W.TILE_BYTES)
+                assert rc == 0 and np.array_equal(got, ref), f"tile {i}"
+                assert np.array_equal(got, vals[i].view(np.uint8))
+            # a file too short for its last block: those tiles get TDBG_E_IO
+            st2 = ctx.read_unfilter(dp, fds, fidx, foff + np.uint64(10**9), size, out_ptrs,
+                                    np.full(len(tiles), W.TILE_BYTES, dtype=np.uint64), cfg=cfg)
+            assert (st2 == 18).all()
+        finally:
+            for fd in fds:
+                os.close(fd)
+
+
+# ---------------------------------------------------------------------------
+# GPU: dense cell-slab copy fused with the D2H
+# ---------------------------------------------------------------------------
+def _dense_tiles(shape_tiles, ext, cell_order, rng, dtype=np.int32):
+    """A dense array of whole tiles (the domain is tile-aligned) and its tiles'
+    cell bytes in the given cell order."""
+    nd = len(ext)
+    full = tuple(t * e for t, e in zip(shape_tiles, ext))
+    A = rng.integers(-2**31, 2**31, full, dtype=np.int64).astype(dtype)
+    tiles, starts = [], []
+    for idx in np.ndindex(*shape_tiles):
+        s = tuple(i * e for i, e in zip(idx, ext))
+        blk = A[tuple(slice(s[d], s[d] + ext[d]) for d in range(nd))]
+        cells = blk.reshape(-1) if cell_order == 0 else np.asfortranarray(blk).T.reshape(-1)
+        tiles.append(np.ascontiguousarray(cells).view(np.uint8))
+        starts.append(s)
+    return A, tiles, np.array(starts, dtype=np.int64)
+
+
+_DENSE = [
+    ((4, 5), (16, 32), (3, 7), (60, 150), 0, 0),
+    ((4, 5), (16, 32), (3, 7), (60, 150), 0, 1),
+    ((4, 5), (16, 32), (0, 0), (63, 159), 1, 0),
+    ((4, 5), (16, 32), (17, 40), (17, 140), 1, 1),
+    ((3,), (1000,), (5,), (2990,), 0, 0),
+    ((2, 3, 4), (8, 4, 16), (1, 2, 3), (14, 10, 60), 0, 0),
+    ((2, 3, 4), (8, 4, 16), (1, 2, 3), (14, 10, 60), 1, 1),
+    ((2, 3, 4), (8, 4, 16), (0, 0, 0), (0, 11, 63), 0, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _DENSE, ids=lambda c: f"t{'x'.join(map(str, c[0]))}_o{c[4]}l{c[5]}")
+def test_dense_read_fused_copy(oracle_mod, case):
+    import torch
+    assert torch.cuda.is_available()
+    from tiledb_amd import engine
+    shape_tiles, ext, lo, hi, cell_order, layout = case
+    rng = np.random.default_rng(sum(ext) + cell_order + 2 * layout)
+    A, raw, starts = _dense_tiles(shape_tiles, ext, cell_order, rng)
+    # C1's pipeline ([BYTESHUFFLE] on INT32) and C5's
+    for ser in (FilterPipeline(65536, [ByteshuffleFilter()]).serialize(), _c5_pipe()):
+        op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.INT32), 4)
+        filt = [np.frombuffer(op.filter_tile(t), dtype=np.uint8) for t in raw]
+        ctx = engine.Context(0)
+        dp = engine.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+        cfg = engine.dense_config(4, ext, lo, hi, cell_order, layout)
+        nb = engine.dense_result_bytes(cfg)
+        result = np.full(nb, 0xAB, dtype=np.uint8)
+        st = ctx.dense_read(dp, filt, starts, cfg, result, batch_bytes=1 << 20)
+        assert not st.any()
+        want = oracle_mod.dense_subarray_cells(raw, starts, ext, 4, lo, hi, cell_order, layout)
+        assert np.array_equal(result, want)
+        sub = A[tuple(slice(l, h + 1) for l, h in zip(lo, hi))]
+        ref = (sub.reshape(-1) if layout == 0 else np.asfortranarray(sub).T.reshape(-1)).view(np.uint8)
+        assert np.array_equal(result, ref)
+
+
+@pytest.mark.gpu
+def test_dense_copy_async_skips_failed_tiles(oracle_mod):
+    """Device-resident copy: a tile whose status is not OK leaves its cells
+    untouched; the others land where copy_fixed_tiles puts them."""
+    import torch
+    from tiledb_amd import engine
+    rng = np.random.default_rng(51)
+    ext, shape_tiles, lo, hi = (16, 32), (3, 3), (2, 5), (40, 90)
+    A, raw, starts = _dense_tiles(shape_tiles, ext, 0, rng)
+    dev = torch.device("cuda", 0)
+    d_tiles = [torch.from_numpy(t.copy()).to(dev) for t in raw]
+    ptrs = torch.tensor([t.data_ptr() for t in d_tiles], dtype=torch.int64, device=dev)
+    d_start = torch.from_numpy(starts.reshape(-1)).to(dev)
+    status = torch.zeros(len(raw), dtype=torch.int32, device=dev)
+    status[4] = 5
+    cfg = engine.dense_config(4, ext, lo, hi)
+    d_res = torch.full((engine.dense_result_bytes(cfg),), 7, dtype=torch.uint8, device=dev)
+    ctx = engine.Context(0)
+    ctx.dense_copy_async(cfg, len(raw), d_start.data_ptr(), ptrs.data_ptr(), d_res.data_ptr(),
+                         d_status=status.data_ptr())
+    torch.cuda.synchronize()
+    got = d_res.cpu().numpy()
+    want = oracle_mod.dense_subarray_cells(raw, starts, ext, 4, lo, hi)
+    # which result bytes come from tile 4: mark its cells and copy the marks
+    marks = [np.full(t.size, 1 if i == 4 else 0, np.uint8) for i, t in enumerate(raw)]
+    mask = oracle_mod.dense_subarray_cells(marks, starts, ext, 4, lo, hi).astype(bool)
+    assert mask.any() and not mask.all()
+    assert np.array_equal(got[~mask], want[~mask])
+    assert (got[mask] == 7).all()

@@ -10,8 +10,10 @@ gathered shards cover every tile exactly once.
 """
 from __future__ import annotations
 
+import argparse
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -55,8 +57,10 @@ def _worker(rank: int, world: int, port: int, q):
         dp = engine.DevicePipeline(W.c5_pipeline_bytes(), 23, 0, 4)
         bufs = [np.frombuffer(tiles[i], dtype=np.uint8).copy() for i in range(lo, hi)]
         outs = [np.zeros(W.TILE_BYTES, dtype=np.uint8) for _ in range(lo, hi)]
+        t0 = time.perf_counter()
         st = engine.unfilter_cpu(dp, [b.ctypes.data for b in bufs], isz[lo:hi],
                                  [o.ctypes.data for o in outs], osz[lo:hi], nthreads=2)
+        el = time.perf_counter() - t0
         assert not st.any()
         digests = np.zeros(len(tiles), dtype=np.int64)
         for k, i in enumerate(range(lo, hi)):
@@ -65,8 +69,20 @@ def _worker(rank: int, world: int, port: int, q):
         t = torch.from_numpy(digests)
         dist.all_reduce(t)  # disjoint shards: the sum is a gather
         slow = bench.max_over_ranks(dist, float(rank + 1), "cpu")
+        # the bench's N = 2 line, from this rank's shard timed on the CPU
+        # entry (stand-in for the GPU timing): max-over-ranks time, total
+        # bytes over ranks, roofline, and rank 0's cpu_baseline
+        packed = np.concatenate(bufs)
+        offs = np.concatenate([[0], np.cumsum(isz[lo:hi])[:-1]]).astype(np.uint64)
+        elapsed = bench.max_over_ranks(dist, el, "cpu")
+        r = dict(elapsed=elapsed, kern_ms=el * 1e3, launch_ms=el * 1e3, b_alg=float(isz[lo:hi].sum() + osz[lo:hi].sum()),
+                 unf=float(osz[lo:hi].sum()), out_bytes=W.TILE_BYTES, fused=hi - lo, fallback=0, streamed=hi - lo,
+                 packed=packed, offs=offs, sizes=isz[lo:hi], steps=1, ntiles=hi - lo)
+        args = argparse.Namespace(config="c5", warmup=0, unique=len(tiles), align=1, e2e_batch_mb=64)
+        line = bench.headline_line(args, W, ["rand"], {"rand": r}, world)
         if rank == 0:
-            q.put((t.numpy().tolist(), cuts.tolist(), slow))
+            line["cpu_baseline"] = bench.cpu_line(engine, dp, r, "c5", "rand", 2, 0.2)
+            q.put((t.numpy().tolist(), cuts.tolist(), slow, line))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -84,7 +100,7 @@ def test_two_rank_shards_cover_every_tile_once():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    digests, cuts, slow = q.get(timeout=240)
+    digests, cuts, slow, line = q.get(timeout=240)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -93,3 +109,51 @@ def test_two_rank_shards_cover_every_tile_once():
     for i in range(len(tiles)):
         assert digests[i] == int(vals[i].view(np.uint32).astype(np.uint64).sum()) + 1
     assert slow == 2.0
+    # the N = 2 line: whole-job value over both ranks, roofline, CPU baseline
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    assert line["roofline"]["bound"] == "hbm" and 0 < line["roofline"]["frac"]
+    cb = line["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0 and cb["unit"] == "GiB/s"
+
+
+class _FakeCuda:
+    def __init__(self, n):
+        self.n, self.dev = n, None
+
+    def device_count(self):
+        return self.n
+
+    def set_device(self, d):
+        self.dev = d
+
+
+class _FakeTorch:
+    def __init__(self, n):
+        self.cuda = _FakeCuda(n)
+
+    @staticmethod
+    def device(kind, idx):
+        return (kind, idx)
+
+
+class _FakeDist:
+    def __init__(self):
+        self.calls = []
+
+    def init_process_group(self, backend, **kw):
+        self.calls.append((backend, kw))
+
+
+def test_init_dist_binds_each_rank_to_its_gpu():
+    """bench.py's RCCL path: one process per GPU, init_process_group('nccl',
+    device_id=cuda:LOCAL_RANK) after set_device(LOCAL_RANK); the gloo
+    rehearsal shares the box's GPUs round-robin and reduces on the CPU."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    d, t = _FakeDist(), _FakeTorch(8)
+    assert bench.init_dist(d, t, {}, 5) == "cuda"
+    assert t.cuda.dev == 5 and d.calls == [("nccl", {"device_id": ("cuda", 5)})]
+    d, t = _FakeDist(), _FakeTorch(1)
+    assert bench.init_dist(d, t, {"TDBG_DIST_BACKEND": "gloo"}, 3) == "cpu"
+    assert t.cuda.dev == 0 and d.calls == [("gloo", {})]

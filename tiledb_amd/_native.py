@@ -77,7 +77,36 @@ SIGNATURES = {
     "tdbg_memcpy_h2d": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
     "tdbg_memcpy_d2h": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
     "tdbg_device_count": (ctypes.c_int, [c_i32p]),
+    "tdbg_context_device": (ctypes.c_int, [c_vp]),
+    "tdbg_host_alloc_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "tdbg_host_free": (ctypes.c_int, [c_vp]),
+    "tdbg_filtered_data_blocks": (ctypes.c_int, [ctypes.c_uint64, c_vp, c_vp, c_vp, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_uint64, c_vp, c_u64p]),
+    "tdbg_read_unfilter_tiles": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, ctypes.c_uint32, c_vp, c_vp,
+                                                c_vp, c_vp, c_vp, ctypes.c_uint32, c_vp, c_i32p]),
+    "tdbg_dense_result_bytes": (ctypes.c_uint64, [c_vp]),
+    "tdbg_dense_copy_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "tdbg_dense_read_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            ctypes.c_uint64, ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
 }
+
+DENSE_MAX_DIMS = 4  # TDBG_DENSE_MAX_DIMS
+
+
+class ReadConfig(ctypes.Structure):
+    """tdbg_read_config (FilteredData block rule + IO threads)."""
+    _fields_ = [("min_batch_size", ctypes.c_uint64), ("max_batch_size", ctypes.c_uint64),
+                ("min_batch_gap", ctypes.c_uint64), ("io_threads", ctypes.c_uint32),
+                ("slots", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class DenseCopyConfig(ctypes.Structure):
+    """tdbg_dense_copy_config (DenseReader::copy_fixed_tiles for one fragment)."""
+    _fields_ = [("dim_num", ctypes.c_uint32), ("cell_size", ctypes.c_uint32),
+                ("cell_order", ctypes.c_uint32), ("layout", ctypes.c_uint32),
+                ("tile_extent", ctypes.c_int64 * DENSE_MAX_DIMS),
+                ("sub_lo", ctypes.c_int64 * DENSE_MAX_DIMS),
+                ("sub_hi", ctypes.c_int64 * DENSE_MAX_DIMS)]
 
 for _name, (_res, _args) in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -21,6 +21,8 @@ NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
           ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
           ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
+          ("tdbg_dense.hip", "tdbg_dense", []),
+          ("tdbg_io.cpp", "tdbg_io", []),
           # CPU entry: host-only C++, product and sum rounded separately
           # (FLOAT_SCALE parity with the reference's x86-64 build)
           ("tdbg_cpu.cpp", "tdbg_cpu", ["-ffp-contract=off"])] +

@@ -54,6 +54,10 @@ extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid,
 extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
+extern "C" hipError_t tdbg_launch_dense_copy(const tdbg_dense_copy_config* cfg, uint64_t ntiles,
+                                             const int64_t* tile_start, const uint8_t* const* tiles,
+                                             const int32_t* status, uint8_t* result, uint32_t grid,
+                                             hipStream_t s);
 extern "C" uint32_t tdbg_fast_grid(uint32_t fast, int cus);
 
 namespace {
@@ -400,6 +404,7 @@ const char* tdbg_status_str(int s) {
     case TDBG_E_DESCRIPTOR: return "Deserialization error; malformed filter pipeline";
     case TDBG_E_DELTA_TYPE: return "Decompression is not yet supported for float datatypes.";
     case TDBG_E_INTERNAL: return "internal: device work queue overflow";
+    case TDBG_E_IO: return "tile read failed (short read or I/O error)";
     default: return "unknown";
   }
 }
@@ -1499,6 +1504,216 @@ int tdbg_unfilter_tiles_multi_gpu(const tdbg_pipeline* p, uint64_t ntiles,
           return fail(st[i], msg);
         }
       return fail(rcs[d], errs[d]);
+    }
+  return TDBG_OK;
+}
+
+int tdbg_context_device(const tdbg_context* c) { return c ? c->device : -1; }
+
+// ---------------------------------------------------------------------------
+// dense cell-slab copy (DenseReader::copy_fixed_tiles, dense_reader.cc:1555-1750)
+// ---------------------------------------------------------------------------
+static bool dense_cfg_ok(const tdbg_dense_copy_config* g) {
+  if (!g || g->dim_num < 1 || g->dim_num > TDBG_DENSE_MAX_DIMS || g->cell_size == 0 || g->cell_order > 1 ||
+      g->layout > 1)
+    return false;
+  for (uint32_t d = 0; d < g->dim_num; d++)
+    if (g->tile_extent[d] <= 0 || g->sub_hi[d] < g->sub_lo[d]) return false;
+  return true;
+}
+
+uint64_t tdbg_dense_result_bytes(const tdbg_dense_copy_config* g) {
+  if (!dense_cfg_ok(g)) return 0;
+  uint64_t n = g->cell_size;
+  for (uint32_t d = 0; d < g->dim_num; d++) n *= (uint64_t)(g->sub_hi[d] - g->sub_lo[d] + 1);
+  return n;
+}
+
+static uint64_t dense_tile_bytes(const tdbg_dense_copy_config* g) {
+  uint64_t n = g->cell_size;
+  for (uint32_t d = 0; d < g->dim_num; d++) n *= (uint64_t)g->tile_extent[d];
+  return n;
+}
+
+int tdbg_dense_copy_async(tdbg_context* c, const tdbg_dense_copy_config* cfg, uint64_t ntiles,
+                          const int64_t* d_tile_start, const uint8_t* const* d_tiles, const int32_t* d_status,
+                          uint8_t* d_result, tdbg_stream stream) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (!dense_cfg_ok(cfg)) return fail(TDBG_E_ARG, "invalid dense copy config");
+  if (ntiles == 0) return TDBG_OK;
+  if (!d_tile_start || !d_tiles || !d_result) return fail(TDBG_E_ARG, "null dense copy arrays");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
+  hipError_t e = tdbg_launch_dense_copy(cfg, ntiles, d_tile_start, d_tiles, d_status, d_result, grid,
+                                        (hipStream_t)stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense copy launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+int tdbg_dense_read_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles, const uint8_t* const* in,
+                         const uint64_t* in_size, const int64_t* tile_start, const tdbg_dense_copy_config* cfg,
+                         uint8_t* result, uint64_t result_size, uint32_t flags, int32_t* host_status,
+                         uint64_t batch_bytes) {
+  if (!c || !p) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!p->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (!dense_cfg_ok(cfg)) return fail(TDBG_E_ARG, "invalid dense copy config");
+  const uint64_t rbytes = tdbg_dense_result_bytes(cfg);
+  if (!result || result_size < rbytes) return fail(TDBG_E_ARG, "result buffer smaller than the subarray");
+  if (ntiles == 0) return TDBG_OK;
+  if (!in || !in_size || !tile_start) return fail(TDBG_E_ARG, "null tile arrays");
+  HIP_OK(hipSetDevice(c->device));
+  if (batch_bytes == 0) batch_bytes = 256ull << 20;
+  const bool cin = (flags & TDBG_HOST_CONTIGUOUS_INPUT) != 0;
+  flags &= ~(TDBG_HOST_CONTIGUOUS_INPUT | TDBG_HOST_CONTIGUOUS_OUTPUT);
+  if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  if (!c->hstream) HIP_OK(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
+  {
+    int rc = order_stream(c, c->cstream);
+    if (rc) return rc;
+  }
+  const uint32_t nd = cfg->dim_num;
+  const uint64_t tb = dense_tile_bytes(cfg);
+  // the device result buffer and the tile starts (kept until the D2H is done)
+  uint8_t* d_result = nullptr;
+  int64_t* d_start = nullptr;
+  HIP_OK(hipMalloc(&d_result, rbytes));
+  hipError_t e0 = hipMalloc(&d_start, ntiles * nd * sizeof(int64_t));
+  if (e0 == hipSuccess) e0 = hipMemcpy(d_start, tile_start, ntiles * nd * sizeof(int64_t), hipMemcpyHostToDevice);
+  if (e0 != hipSuccess) {
+    (void)hipFree(d_result);
+    if (d_start) (void)hipFree(d_start);
+    return fail(TDBG_E_DEVICE, std::string("dense read setup: ") + hipGetErrorString(e0));
+  }
+  // batches bounded by bytes on both sides; two staging slots alternate
+  std::vector<uint64_t> cuts{0};
+  uint64_t bi = 0, bo = 0;
+  for (uint64_t i = 0; i < ntiles; i++) {
+    if (i > cuts.back() && (bi + in_size[i] > batch_bytes || bo + tb > batch_bytes)) {
+      cuts.push_back(i);
+      bi = bo = 0;
+    }
+    bi += in_size[i];
+    bo += tb;
+  }
+  cuts.push_back(ntiles);
+  std::vector<int32_t> st(ntiles, 0);
+  int rc = TDBG_OK;
+  bool used[2] = {false, false};
+  for (size_t b = 0; b + 1 < cuts.size() && rc == TDBG_OK; b++) {
+    auto& S = c->st[b % 2];
+    const uint64_t lo = cuts[b], hi = cuts[b + 1], nt = hi - lo;
+    if (used[b % 2]) {  // the slot's previous batch (kernels + status copy) is done
+      if (hipEventSynchronize(S.done) != hipSuccess) { rc = fail(TDBG_E_DEVICE, "dense read: event wait"); break; }
+    }
+    const uint64_t ib = in_dev_offsets(in, in_size, lo, hi, nullptr, cin);
+    rc = stage_reserve(S, ib + 16, nt * tb + 16, nt);
+    if (rc) break;
+    const uint8_t** hp = S.h_ptrs;
+    uint64_t* hs = (uint64_t*)(hp + nt);
+    uint8_t** ho = (uint8_t**)(hs + nt);
+    uint64_t* hos = (uint64_t*)(ho + nt);
+    in_dev_offsets(in, in_size, lo, hi, (uint64_t*)hp, cin);
+    for (uint64_t i = lo; i < hi; i++) {
+      hp[i - lo] = S.d_in + (uint64_t)(uintptr_t)hp[i - lo];
+      hs[i - lo] = in_size[i];
+      ho[i - lo] = S.d_out + (i - lo) * tb;
+      hos[i - lo] = tb;
+    }
+    hipError_t e = hipMemcpyAsync(S.d_ptrs, hp, nt * 32, hipMemcpyHostToDevice, c->hstream);
+    if (e != hipSuccess) { rc = fail(TDBG_E_DEVICE, "dense read: pointer copy"); break; }
+    rc = copy_ranges(c->hstream, lo, hi, in, in_size, S.d_in, true, nullptr, cin);
+    if (rc) break;
+    if (hipEventRecord(S.h2d, c->hstream) != hipSuccess || hipStreamWaitEvent(c->cstream, S.h2d, 0) != hipSuccess) {
+      rc = fail(TDBG_E_DEVICE, "dense read: stream ordering");
+      break;
+    }
+    const uint8_t* const* dp = (const uint8_t* const*)S.d_ptrs;
+    const uint64_t* ds = (const uint64_t*)(dp + nt);
+    uint8_t* const* dop = (uint8_t* const*)(ds + nt);
+    const uint64_t* dos = (const uint64_t*)(dop + nt);
+    rc = ensure_status(c, nt);
+    if (rc) break;
+    rc = launch(c, p, nt, dp, ds, dop, dos, flags, S.d_stat, c->d_need, nullptr, c->cstream, false);
+    if (rc) break;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, (uint64_t)c->cus * 8);
+    e = tdbg_launch_dense_copy(cfg, nt, d_start + lo * nd, (const uint8_t* const*)dop, S.d_stat, d_result, grid,
+                               c->cstream);
+    if (e != hipSuccess) { rc = fail(TDBG_E_DEVICE, std::string("dense copy launch: ") + hipGetErrorString(e)); break; }
+    e = hipMemcpyAsync(st.data() + lo, S.d_stat, nt * 4, hipMemcpyDeviceToHost, c->cstream);
+    if (e == hipSuccess) e = hipEventRecord(S.done, c->cstream);
+    if (e != hipSuccess) { rc = fail(TDBG_E_DEVICE, "dense read: status copy"); break; }
+    used[b % 2] = true;
+  }
+  // the one D2H: the subarray's cells
+  if (rc == TDBG_OK) {
+    hipError_t e = hipMemcpyAsync(result, d_result, rbytes, hipMemcpyDeviceToHost, c->cstream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->cstream);
+    if (e != hipSuccess) rc = fail(TDBG_E_DEVICE, std::string("dense read D2H: ") + hipGetErrorString(e));
+  } else {
+    (void)hipStreamSynchronize(c->cstream);
+  }
+  (void)hipFree(d_result);
+  (void)hipFree(d_start);
+  if (rc) return rc;
+  c->tiles_unfiltered += ntiles;
+  // tiles that needed bigger scratch: their cells are re-copied through the sync path
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (st[i] == TDBG_E_SCRATCH) {
+      std::vector<uint8_t> tile(tb);
+      uint8_t* outp = tile.data();
+      int32_t one = 0;
+      int r2 = unfilter_host(c, p, 1, in + i, in_size + i, &outp, &tb, nullptr, flags, &one, 0);
+      st[i] = one;
+      if (r2 == TDBG_OK && one == TDBG_OK) {
+        // host-side slab copy of this one tile (rare path)
+        tdbg_dense_copy_config g = *cfg;
+        std::vector<int64_t> cc(nd);
+        const int64_t* s0 = tile_start + i * nd;
+        int64_t lo2[TDBG_DENSE_MAX_DIMS], len[TDBG_DENSE_MAX_DIMS];
+        bool empty = false;
+        uint64_t ncell = 1;
+        for (uint32_t d = 0; d < nd; d++) {
+          lo2[d] = std::max(s0[d], g.sub_lo[d]);
+          const int64_t hi2 = std::min(s0[d] + g.tile_extent[d] - 1, g.sub_hi[d]);
+          if (hi2 < lo2[d]) empty = true;
+          len[d] = hi2 - lo2[d] + 1;
+          if (!empty) ncell *= (uint64_t)len[d];
+        }
+        if (empty) continue;
+        for (uint64_t k = 0; k < ncell; k++) {
+          uint64_t r = k;
+          for (uint32_t d = 0; d < nd; d++) {
+            cc[d] = (int64_t)(r % (uint64_t)len[d]);
+            r /= (uint64_t)len[d];
+          }
+          uint64_t si = 0, di = 0;
+          auto L = [&](const int64_t* ext, bool row, bool tilecoord) {
+            uint64_t x = 0;
+            if (row) {
+              for (uint32_t d = 0; d < nd; d++)
+                x = x * (uint64_t)ext[d] + (uint64_t)(lo2[d] + cc[d] - (tilecoord ? s0[d] : g.sub_lo[d]));
+            } else {
+              for (int d = (int)nd - 1; d >= 0; d--)
+                x = x * (uint64_t)ext[d] + (uint64_t)(lo2[d] + cc[d] - (tilecoord ? s0[d] : g.sub_lo[d]));
+            }
+            return x;
+          };
+          int64_t sub_ext[TDBG_DENSE_MAX_DIMS];
+          for (uint32_t d = 0; d < nd; d++) sub_ext[d] = g.sub_hi[d] - g.sub_lo[d] + 1;
+          si = L(g.tile_extent, g.cell_order == 0, true);
+          di = L(sub_ext, g.layout == 0, false);
+          memcpy(result + di * g.cell_size, tile.data() + si * g.cell_size, g.cell_size);
+        }
+      }
+    }
+  if (host_status) memcpy(host_status, st.data(), ntiles * 4);
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (st[i]) {
+      char msg[160];
+      snprintf(msg, sizeof(msg), "tile %llu: %s", (unsigned long long)i, tdbg_status_str(st[i]));
+      return fail(st[i], msg);
     }
   return TDBG_OK;
 }

@@ -439,7 +439,8 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
 #endif
 
 // ABL: timing ablations (outputs not meaningful): 1 parse only a workgroup's
-// first tile (identical rand tiles), 2 one DMA unit per job plane, 3 no stores
+// first tile (identical rand tiles), 2 one DMA unit per job plane, 3 no
+// stores, 4 no jobs (walk, prefix, parse and barriers only)
 template <bool SGN, int ABL>
 __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(const KParams kp) {
   __shared__ Lds L;
@@ -487,7 +488,7 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
     if (hn && ABL != 1) prefix_dma(L, nxt, w, l);
     pf_waited = false;
     if (ok) {
-      tile_jobs<SGN, ABL>(L, cur, w, l, wsh);
+      if (ABL != 4) tile_jobs<SGN, ABL>(L, cur, w, l, wsh);
       pf_waited = true;  // the first job's wait covered the prefix (older)
       ok_tiles++;
       if (threadIdx.x == 0 && kp.status) kp.status[cur.t] = TDBG_OK;
@@ -519,6 +520,7 @@ extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t g
   auto k = sgn ? (abl == 1   ? unfilter_stream_raw_kernel<true, 1>
                   : abl == 2 ? unfilter_stream_raw_kernel<true, 2>
                   : abl == 3 ? unfilter_stream_raw_kernel<true, 3>
+                  : abl == 4 ? unfilter_stream_raw_kernel<true, 4>
                              : unfilter_stream_raw_kernel<true, 0>)
                : unfilter_stream_raw_kernel<false, 0>;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);

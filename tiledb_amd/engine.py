@@ -368,6 +368,52 @@ class Context:
                                                 self._stream(stream)), "tdbg_add_extra_offsets_async")
         torch.cuda.synchronize(batch.d_out.device)
 
+    def read_unfilter(self, dp: DevicePipeline, fds, file_idx, file_offset, size, out_ptrs, out_sizes,
+                       flags: int = 0, cfg=None) -> np.ndarray:
+        """tdbg_read_unfilter_tiles: FilteredData-style block reads from the open
+        files `fds` -> H2D -> unfilter -> D2H into out_ptrs; per-tile statuses."""
+        n = int(np.asarray(size).size)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        fd = np.ascontiguousarray(fds, dtype=np.int32)
+        fi = np.ascontiguousarray(file_idx, dtype=np.uint32)
+        fo = np.ascontiguousarray(file_offset, dtype=np.uint64)
+        sz = np.ascontiguousarray(size, dtype=np.uint64)
+        op = np.ascontiguousarray(out_ptrs, dtype=np.uint64)
+        osz = np.ascontiguousarray(out_sizes, dtype=np.uint64)
+        rc = lib.tdbg_read_unfilter_tiles(self.h, dp.h, n, fd.ctypes.data, fd.size, fi.ctypes.data, fo.ctypes.data,
+                                          sz.ctypes.data, op.ctypes.data, osz.ctypes.data, flags,
+                                          ctypes.byref(cfg) if cfg is not None else None,
+                                          st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if rc and not st[:n].any():
+            _check(rc, "tdbg_read_unfilter_tiles")
+        return st[:n]
+
+
+    def dense_read(self, dp: DevicePipeline, tiles, tile_start, cfg, result: np.ndarray, flags: int = 0,
+                    batch_bytes: int = 0) -> np.ndarray:
+        """tdbg_dense_read_host: filtered host tiles -> unfilter -> cell-slab copy
+        on the device -> one D2H of the subarray into `result` (uint8 array)."""
+        bufs = [np.ascontiguousarray(t, dtype=np.uint8).reshape(-1) for t in tiles]
+        n = len(bufs)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        ip = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+        isz = np.array([b.size for b in bufs], dtype=np.uint64)
+        ts = np.ascontiguousarray(tile_start, dtype=np.int64)
+        assert result.dtype == np.uint8 and result.flags.c_contiguous
+        rc = lib.tdbg_dense_read_host(self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data, ts.ctypes.data,
+                                      ctypes.byref(cfg), result.ctypes.data, result.size, flags,
+                                      st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), batch_bytes)
+        if rc and not st[:n].any():
+            _check(rc, "tdbg_dense_read_host")
+        return st[:n]
+
+
+    def dense_copy_async(self, cfg, ntiles: int, d_tile_start, d_tiles, d_result, d_status=None, stream=None) -> None:
+        """tdbg_dense_copy_async on device pointers (ints)."""
+        _check(lib.tdbg_dense_copy_async(self.h, ctypes.byref(cfg), ntiles, d_tile_start, d_tiles,
+                                         d_status if d_status else None, d_result, self._stream(stream)),
+               "tdbg_dense_copy_async")
+
 
 def unfilter_cpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, nthreads: int = 0,
                  offsets_tiles: bool = False) -> np.ndarray:
@@ -430,3 +476,53 @@ def device_count() -> int:
     n = ctypes.c_int32()
     _check(lib.tdbg_device_count(ctypes.byref(n)), "tdbg_device_count")
     return int(n.value)
+
+
+# ---------------------------------------------------------------------------
+# the steps either side of the path
+# ---------------------------------------------------------------------------
+def filtered_data_blocks(file_idx, file_offset, size, min_batch_size: int = 20971520,
+                         max_batch_size: int = 104857600, min_batch_gap: int = 512000) -> np.ndarray:
+    """FilteredData blocks (filtered_data.h:503-540) of tiles in result-tile
+    order: the first tile of every block, then ntiles."""
+    fi = np.ascontiguousarray(file_idx, dtype=np.uint32)
+    fo = np.ascontiguousarray(file_offset, dtype=np.uint64)
+    sz = np.ascontiguousarray(size, dtype=np.uint64)
+    first = np.zeros(fi.size + 1, dtype=np.uint64)
+    nb = ctypes.c_uint64()
+    _check(lib.tdbg_filtered_data_blocks(fi.size, fi.ctypes.data, fo.ctypes.data, sz.ctypes.data, min_batch_size,
+                                         max_batch_size, min_batch_gap, first.ctypes.data, ctypes.byref(nb)),
+           "tdbg_filtered_data_blocks")
+    n = int(nb.value)
+    return np.concatenate([first[:n], [fi.size]]).astype(np.uint64) if fi.size else np.zeros(1, np.uint64)
+
+
+class HostBuffer:
+    """Pinned host memory on a device's NUMA node (tdbg_host_alloc_local)."""
+
+    def __init__(self, device: int, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib.tdbg_host_alloc_local(device, nbytes, ctypes.byref(p)), "tdbg_host_alloc_local")
+        self.ptr = int(p.value or 0)
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(self.ptr))[:nbytes]
+
+    def __del__(self, _free=lib.tdbg_host_free, _down=_SHUTDOWN):
+        if getattr(self, "ptr", 0) and not _down:
+            _free(ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+
+def dense_config(cell_size: int, tile_extent, sub_lo, sub_hi, cell_order: int = 0,
+                 layout: int = 0) -> "_native.DenseCopyConfig":
+    """tdbg_dense_copy_config: row-major = 0, col-major = 1."""
+    g = _native.DenseCopyConfig()
+    nd = len(tile_extent)
+    g.dim_num, g.cell_size, g.cell_order, g.layout = nd, cell_size, cell_order, layout
+    for d in range(nd):
+        g.tile_extent[d], g.sub_lo[d], g.sub_hi[d] = int(tile_extent[d]), int(sub_lo[d]), int(sub_hi[d])
+    return g
+
+
+def dense_result_bytes(cfg) -> int:
+    return int(lib.tdbg_dense_result_bytes(ctypes.byref(cfg)))

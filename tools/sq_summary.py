@@ -33,9 +33,15 @@ def main(out, cfg, var, tiles=12500):
     if "SQ_WAVE_CYCLES" in c:
         w = c["SQ_WAVE_CYCLES"]
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
-                  "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
+                  "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_SCA"):
             if k in c:
                 der[k + "_share_of_wave_cycles"] = round(c[k] / w, 4)
+    # per CU: SALU issues one instruction per cycle for the whole CU, so
+    # SALU instructions / CU vs the kernel's cycles is the scalar unit's load
+    if "SQ_INSTS_SALU" in c:
+        der["SQ_INSTS_SALU_per_CU"] = round(c["SQ_INSTS_SALU"] / 256, 1)
+    if "SQ_INSTS_VALU" in c:
+        der["SQ_INSTS_VALU_per_SIMD"] = round(c["SQ_INSTS_VALU"] / 1024, 1)
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
         if k in c:
             der[k + "_per_tile"] = round(c[k] / tiles, 1)
