@@ -327,6 +327,11 @@ int tdbg_context_stream_stats(const tdbg_context* ctx, uint64_t* stream_tiles);
 /* Of those, the tiles the raw-DoubleDelta streaming kernel took (C5 tiles
  * whose DD stage stored the values raw, tdbg_stream_raw.hip). */
 int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles);
+/* Forward direction: tiles the LDS-resident kernel for [BYTESHUFFLE,
+ * DOUBLE_DELTA, BWR(256)] on INT32 / UINT32 64 KiB tiles filtered
+ * (tdbg_forward_stream.hip; the others run on the general forward kernel).
+ * Cumulative; waits for the context's last launch. */
+int tdbg_context_forward_stream_stats(const tdbg_context* c, uint64_t* tiles);
 
 /* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on
  * ctx (fused/general kernel + fixup), from the hipEvents that

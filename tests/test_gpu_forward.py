@@ -126,3 +126,47 @@ def test_forward_full_size_c5(eng, ctx, oracle_mod):
     case = Case("c5_full", P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256)), Datatype.INT32, 4,
                 tiles)
     forward_parity(eng, ctx, oracle_mod, case)
+
+
+def test_forward_stream_c5_kernel(eng, ctx, oracle_mod):
+    """The LDS-resident C5 forward kernel (tdbg_forward_stream.hip): every DD
+    bit size (raw and coded, 1..32), active / ramp / rand tiles, INT32 and
+    UINT32, bit-exact with the oracle, and proven to have filtered them
+    (tdbg_context_forward_stream_stats)."""
+    import workloads as W
+    from tests.cases import c5_tiles, P, DD, Case
+    from tests.test_gpu_stream import step_values
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
+    rng = np.random.default_rng(61)
+    vals = [step_values(b, rng) for b in range(1, 33)]
+    vals += [W.c5_values(v, k, rng) for v in ("active", "ramp", "rand") for k in range(3)]
+    vals.append(np.zeros(16384, dtype=np.int32))
+    vals.append(np.full(16384, -7, dtype=np.int32))
+    pipe = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
+    for dt, cast in ((Datatype.INT32, np.int32), (Datatype.UINT32, np.uint32)):
+        tiles = [np.ascontiguousarray(v).view(cast).view(np.uint8) for v in vals]
+        f0 = ctx.forward_stream_tiles()
+        forward_parity(eng, ctx, oracle_mod, Case(f"c5fs_{int(dt)}", pipe, dt, 4, tiles))
+        assert ctx.forward_stream_tiles() - f0 == len(tiles)
+
+
+def test_forward_stream_c5_declines(eng, ctx, oracle_mod):
+    """Tiles the C5 forward kernel does not take (not 64 KiB, another BWR
+    window, a different max chunk) run on the general forward kernel with
+    the oracle's bytes; a 64 KiB tile next to them is still taken."""
+    import workloads as W
+    from tests.cases import P, DD, Case
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
+    rng = np.random.default_rng(62)
+    full = W.c5_values("active", 1, rng).view(np.uint8)
+    odd = [full[:4000].copy(), full[:65532].copy(), np.concatenate([full, full[:400]])]
+    pipe = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
+    f0 = ctx.forward_stream_tiles()
+    forward_parity(eng, ctx, oracle_mod, Case("c5fs_odd", pipe, Datatype.INT32, 4, odd + [full]))
+    assert ctx.forward_stream_tiles() - f0 == 1
+    f0 = ctx.forward_stream_tiles()
+    forward_parity(eng, ctx, oracle_mod, Case("c5fs_w512", P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(512)),
+                                              Datatype.INT32, 4, [full, full]))
+    case = Case("c5fs_chunk", pipe, Datatype.INT32, 4, [full, full], max_chunk=16384)
+    forward_parity(eng, ctx, oracle_mod, case)
+    assert ctx.forward_stream_tiles() == f0

@@ -66,6 +66,7 @@ SIGNATURES = {
     "tdbg_context_path_stats": (ctypes.c_int, [c_vp, c_u64p, c_u64p, c_u64p]),
     "tdbg_context_stream_stats": (ctypes.c_int, [c_vp, c_u64p]),
     "tdbg_context_stream_raw_stats": (ctypes.c_int, [c_vp, c_u64p]),
+    "tdbg_context_forward_stream_stats": (ctypes.c_int, [c_vp, c_u64p]),
     "tdbg_context_last_kernel_ms": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "tdbg_context_time_launches": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
     "tdbg_context_launch_times": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint32,

@@ -21,6 +21,8 @@ NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
           ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
           ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
+          ("tdbg_stream_small.hip", "tdbg_stream_small", []),
+          ("tdbg_forward_stream.hip", "tdbg_forward_stream", []),
           ("tdbg_dense.hip", "tdbg_dense", []),
           ("tdbg_io.cpp", "tdbg_io", []),
           # CPU entry: host-only C++, product and sum rounded separately
@@ -29,7 +31,7 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
 HOST_ONLY = {"tdbg_cpu.cpp"}
-NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip"}  # checked with -Rpass-analysis
+NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip"}  # checked with -Rpass-analysis
 HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h"]
 
 

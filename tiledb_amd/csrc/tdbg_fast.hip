@@ -509,6 +509,82 @@ __device__ __forceinline__ bool f_bitshuffle(FastLds& L, View& cur, uint32_t& mo
     return true;
   }
   const uint8_t* X = L.X;
+  if (TS == 4 && final && n % 8192 == 0) {
+    // Whole 8192-B blocks of 4-byte elements (C2 / C2i): a block is 32 bit
+    // rows of 256 B (row 8b + k = bit k of byte b of every element), and
+    // thread t' of the block's wave owns groups 4t'..4t'+3 (elements
+    // 32t'..32t'+31): one dword per row holds its four groups' bytes.  Per
+    // byte plane b, two 4x4 byte transposes of the 8 row dwords give each
+    // group's 64-bit bit matrix, transpose8x8 turns it into the 8 elements'
+    // byte b, and two more 4x4 transposes per group assemble the elements.
+    // 32 LDS reads per thread instead of 128 byte reads.  The 128 output
+    // bytes go back in place, swizzled, behind a barrier, and leave with
+    // lane-consecutive 16-B stores (whole lines: the direct lane-strided
+    // stores cost 1.4x the output bytes in HBM writes).
+    const uint32_t t = tid_(), blk = t >> 6, tq = t & 63;
+    const bool act = blk < n / 8192;  // n <= XCAP: at most 8 blocks, one per wave
+    auto tr4 = [](uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t (&w)[4]) {
+      const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
+      const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
+      const uint32_t c = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+      const uint32_t d = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+      w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+      w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+      w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
+    };
+    uint32_t E[4][8];  // group j: output dwords 0..7
+    auto body = [&](auto AL) {
+      const uint32_t rb = base + 8192 * blk + 4 * tq;
+      uint64_t y[4][4];  // [group j][plane b]
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        uint32_t D[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint32_t a = rb + (8 * b + k) * 256;
+          D[k] = decltype(AL)::value ? *(const uint32_t*)(X + a) : lds32(X, a);
+        }
+        uint32_t lo[4], hi[4];
+        tr4(D[0], D[1], D[2], D[3], lo);
+        tr4(D[4], D[5], D[6], D[7], hi);
+#pragma unroll
+        for (int j = 0; j < 4; j++) y[j][b] = transpose8x8(((uint64_t)hi[j] << 32) | lo[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        uint32_t e0[4], e1[4];
+        tr4((uint32_t)y[j][0], (uint32_t)y[j][1], (uint32_t)y[j][2], (uint32_t)y[j][3], e0);
+        tr4((uint32_t)(y[j][0] >> 32), (uint32_t)(y[j][1] >> 32), (uint32_t)(y[j][2] >> 32),
+            (uint32_t)(y[j][3] >> 32), e1);
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          E[j][m] = e0[m];
+          E[j][4 + m] = e1[m];
+        }
+      }
+    };
+    if (act) {
+      if ((base & 3) == 0) body(std::true_type{});  // (uniform) rows dword-aligned
+      else body(std::false_type{});
+    }
+    __syncthreads();  // every row read before the elements overwrite them
+    if (act) {
+      // thread bytes [8192 blk + 128 t', +128) = units U0 + i, U0 = 512 blk + 8 t'
+      const uint32_t u0 = 512 * blk + 8 * tq;
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        *(uint4*)(L.X + 16 * (u0 + (i ^ (tq & 7)))) =
+            make_uint4(E[i >> 1][4 * (i & 1)], E[i >> 1][4 * (i & 1) + 1], E[i >> 1][4 * (i & 1) + 2],
+                       E[i >> 1][4 * (i & 1) + 3]);
+    }
+    __syncthreads();
+    cur.base = 0;
+    cur.n = n;
+    cur.swz = 1;
+    final_copy(L, cur, gout);
+    return true;
+  }
   constexpr int UB = 8 * TS < 16 ? 16 : 8 * TS;  // unit = whole 8-element groups
   constexpr int GPU_ = UB / (8 * TS);             // groups per unit
   drive<UB>(L, n, final, gout, [&](uint32_t u, uint32_t (&w)[UB / 4]) {

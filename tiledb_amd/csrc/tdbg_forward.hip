@@ -739,7 +739,12 @@ __global__ void __launch_bounds__(FNT_F) filter_tiles_kernel(const KParams kp) {
   sl.md[0] = base + 2ull * kp.slot_cap;
   sl.md[1] = sl.md[0] + kp.md_cap;
   sl.tab = (uint64_t*)(sl.md[1] + kp.md_cap);
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
+  uint64_t ntl = kp.ntiles;
+  if (kp.ntiles_dev) {  // the LDS-resident forward kernel's queue (tdbg_forward_stream.hip)
+    const uint64_t c = (uint32_t)__builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
+    ntl = c < ntl ? c : ntl;
+  }
+  for (uint64_t j = blockIdx.x; j < ntl; j += gridDim.x) {
     const uint64_t t = kp.tile_list ? kp.tile_list[j] : j;
     const uint8_t* in = kp.in[t];
     const uint64_t size = kp.in_size[t];

@@ -1,0 +1,396 @@
+// tdbg_forward_stream.hip -- forward ("filter") direction of the headline
+// pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte
+// integers, one 64 KiB tile = one chunk (the write path WriterBase::
+// filter_tile -> FilterPipeline::run_forward, writer_base.cc:870-915,
+// filter_pipeline.cc:208-369), LDS-resident, gfx950.
+//
+// The general forward kernel (tdbg_forward.hip) runs every filter through a
+// global scratch slot with byte-granular accesses.  Here one 512-thread
+// workgroup owns a tile and the chunk never leaves the CU until its filtered
+// image is stored:
+//
+//   * Byteshuffle (byteshuffle_filter.cc:60-89): thread T loads the 16-B
+//     units 8T..8T+7 (values 32T..32T+31) and two units before them; a 4x4
+//     byte transpose of a unit gives the unit's dword in each of the four
+//     byte planes, so the thread holds positions 8T-2..8T+7 of every plane
+//     of the shuffled stream s (int32, 16,384 values) in registers.
+//   * DoubleDelta (dd_compressor.cc:211-312): the bit size is the bit length
+//     of max(|d1|, |dd_i|) over the tile (one workgroup max); codes (sign,
+//     then bitsize magnitude bits, MSB first in little-endian u64 words) are
+//     OR-ed into the DD output in LDS at their bit offsets, or the values are
+//     stored raw (bitsize >= 31).  The compression filter's metadata part
+//     (the byteshuffle header: two int32) becomes the 17-byte DD part before
+//     it (compression_filter.cc:240-301).
+//   * BWR (bit_width_reduction_filter.cc:110-280, 406-447): 16 lanes per
+//     256-B window read its 64 elements once into registers; min / max give
+//     the window's width; an exclusive workgroup scan of the compressed
+//     sizes places every window; the compressed bytes are written in place
+//     below the DD output (a window's output never reaches past its own
+//     input), next to the metadata and tile header, so the whole filtered
+//     tile is one contiguous LDS image.
+//   * The image leaves with lane-consecutive 16-B stores.
+//
+// The LDS image: DD-output byte x at LDS byte DELTA + x (DELTA = 2 mod 4, so
+// the DD words -- DD-output byte 34 + 8q -- are dword aligned); compressed
+// data byte x at X0 + x (X0 = DELTA - 2); tile header and metadata right
+// below X0.  ~71 KB: two workgroups per CU.
+//
+// Tiles of any other shape (size, alignment, capacity) are queued (KParams::
+// fbq) for the general forward kernel, which runs on the queue right after,
+// so every status and byte stays the oracle's (tests/test_gpu_forward.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../include/tiledb_amd.h"
+#include "tdbg_desc.h"
+#include "tdbg_device.h"
+
+namespace tdbg {
+namespace fws {
+
+constexpr int NT = 512;
+constexpr int NWV = NT / 64;
+constexpr uint32_t NV = 16384;              // int32 values per tile
+constexpr uint32_t TB = NV * 4;             // tile bytes
+constexpr uint32_t NWMAX = 257;             // BWR windows over <= 65,562 DD-output bytes
+constexpr uint32_t MLMAX = 8 + 9 * NWMAX + 24;
+constexpr uint32_t DELTA = 2370;            // >= 22 + MLMAX, = 2 mod 4
+constexpr uint32_t X0 = DELTA - 2;          // compressed data byte 0
+constexpr uint32_t DOUT_MAX = 17 + 9 + TB;  // DD output bytes (raw)
+constexpr uint32_t BDW = (DELTA + DOUT_MAX + 320 + 15) / 16 * 4;  // image dwords (+ reads past the last window)
+constexpr uint32_t WD0 = (DELTA + 34) / 4;  // LDS dword of DD word 0
+constexpr uint32_t PASSES = (NWMAX + NT / 16 - 1) / (NT / 16);  // BWR window passes (9)
+static_assert(DELTA % 4 == 2 && X0 >= 20 + MLMAX, "LDS image layout");
+
+struct Lds {
+  uint32_t B[BDW];
+  uint32_t wcs[NWMAX + 7];   // window compressed bytes, then (after the scan) its data offset
+  uint32_t wkind[NWMAX + 7]; // 0: 8-bit, 1: 16-bit, 2: raw
+  int32_t wmin[NWMAX + 7];
+  uint64_t red[NWV];
+  uint32_t scan[NWV];
+};
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u g_cu4;
+typedef __attribute__((address_space(1))) v4u g_u4;
+
+__device__ __forceinline__ void tr4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t (&w)[4]) {
+  // w[d] byte k = p_k byte d
+  const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
+  const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
+  const uint32_t c = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+  const uint32_t d = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+  w[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+  w[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+  w[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+  w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
+}
+
+__device__ __forceinline__ void lds_byte(Lds& L, uint32_t o, uint32_t v) { ((uint8_t*)L.B)[o] = (uint8_t)v; }
+__device__ __forceinline__ void lds_u32b(Lds& L, uint32_t o, uint32_t v) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) lds_byte(L, o + i, v >> (8 * i));
+}
+
+template <bool SGN>
+__device__ __forceinline__ int64_t ext32(uint32_t v) {
+  return SGN ? (int64_t)(int32_t)v : (int64_t)v;
+}
+__device__ __forceinline__ uint64_t uabs(int64_t v) { return v < 0 ? 0ull - (uint64_t)v : (uint64_t)v; }
+
+// 16-lane group reductions (lanes of one BWR window)
+template <bool SGN>
+__device__ __forceinline__ void grp_minmax(int64_t& mn, int64_t& mx) {
+#pragma unroll
+  for (int d = 8; d >= 1; d >>= 1) {
+    const int64_t a = __shfl_xor(mn, d, 16), b = __shfl_xor(mx, d, 16);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+}
+
+template <bool SGN>
+__global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams kp) {
+  __shared__ Lds L;
+  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
+    // thread index opaque to the optimizer: the unrolled per-thread index
+    // math is tile-invariant, and hoisting it out of the tile loop pins (and
+    // spills) dozens of registers
+    uint32_t T = threadIdx.x;
+    asm volatile("" : "+v"(T));
+    const uint32_t l = T & 63, w = __builtin_amdgcn_readfirstlane(T >> 6);
+    const uint64_t t = j;
+    const uint8_t* in = kp.in[t];
+    uint8_t* out = kp.out[t];
+    const uint64_t isz = kp.in_size[t], cap = kp.out_size[t];
+    // this kernel's tile shape; anything else goes to the general kernel
+    const bool shape = isz == TB && (((uintptr_t)in) & 15) == 0 && (((uintptr_t)out) & 15) == 0 && cap >= 64;
+    bool ok = shape;
+    __syncthreads();  // B0: the last tile's image is stored (LDS free)
+    if (shape) {
+      // ---- zero the DD word region (codes are OR-ed in) ----
+      static_assert(BDW % 4 == 0, "16-B zeroing");
+      for (uint32_t d = (WD0 & ~3u) + 4 * T; d < BDW; d += 4 * NT) *(v4u*)(L.B + d) = v4u{0u, 0u, 0u, 0u};
+      // ---- loads: units 8T..8T+7 and the two before (wrapping into the last
+      // plane's end for T = 0) ----
+      const g_cu4* src = (const g_cu4*)in;
+      v4u U[10];
+#pragma unroll
+      for (int i = 0; i < 10; i++) U[i] = src[(8 * T + i - 2) & 4095u];
+      // S[i][k]: position 8T + i - 2 of plane k (for T = 0 and i < 2: plane k-1's end)
+      uint32_t S[10][4];
+#pragma unroll
+      for (int i = 0; i < 10; i++) tr4(U[i].x, U[i].y, U[i].z, U[i].w, S[i]);
+      if (T == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          S[i][3] = S[i][2];
+          S[i][2] = S[i][1];
+          S[i][1] = S[i][0];
+          S[i][0] = 0;  // (positions -2, -1 do not exist)
+        }
+      }
+      // ---- DoubleDelta bit size: max(|d1|, |dd_i|), i >= 2 ----
+      uint64_t mx = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 2; i < 10; i++) {
+          const uint32_t P = 4096 * k + 8 * T + i - 2;
+          const int64_t d = ext32<SGN>(S[i][k]) - ext32<SGN>(S[i - 1][k]);
+          const int64_t dp = ext32<SGN>(S[i - 1][k]) - ext32<SGN>(S[i - 2][k]);
+          const uint64_t a = P >= 2 ? uabs(d - dp) : P == 1 ? uabs(d) : 0ull;
+          mx = a > mx ? a : mx;
+        }
+#pragma unroll
+      for (int dd = 32; dd >= 1; dd >>= 1) {
+        const uint64_t y = __shfl_xor(mx, dd, 64);
+        mx = y > mx ? y : mx;
+      }
+      if (l == 0) L.red[w] = mx;
+      __syncthreads();  // B1
+      mx = 0;
+#pragma unroll
+      for (int v = 0; v < NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
+      const uint32_t bitsize = mx ? 64 - __builtin_clzll(mx) : 1;  // do { ++b; m >>= 1; } while (m)
+      const bool raw = bitsize >= 31;
+      const uint32_t cb = bitsize + 1;
+      const uint32_t words = raw ? 0u : ((NV - 2) * cb + 63) / 64;
+      const uint32_t cl1 = raw ? 9 + TB : 17 + 8 * words;
+      const uint32_t Ld = 17 + cl1;  // BWR input bytes
+      // ---- the DD output ----
+      if (T == 0) {
+        // md part (the byteshuffle header [1][65536] as two int32):
+        // [bitsize 0][u64 2][1][65536]; data part header [bitsize][u64 16384]
+        lds_byte(L, DELTA, 0);
+        lds_u32b(L, DELTA + 1, 2);
+        lds_u32b(L, DELTA + 5, 0);
+        lds_u32b(L, DELTA + 9, 1);
+        lds_u32b(L, DELTA + 13, TB);
+        lds_byte(L, DELTA + 17, bitsize);
+        lds_u32b(L, DELTA + 18, NV);
+        lds_u32b(L, DELTA + 22, 0);
+      }
+      // s0, s1 (x0, x1; or the first raw values) at DD-output 26 = dword 599
+      if (raw) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+          for (int i = 2; i < 10; i++) L.B[(DELTA + 26) / 4 + 4096 * k + 8 * T + i - 2] = S[i][k];
+      } else {
+        if (T == 0) {
+          L.B[(DELTA + 26) / 4] = S[2][0];
+          L.B[(DELTA + 30) / 4] = S[3][0];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+          for (int i = 2; i < 10; i++) {
+            const uint32_t P = 4096 * k + 8 * T + i - 2;
+            if (P < 2) continue;
+            const int64_t dd = (ext32<SGN>(S[i][k]) - ext32<SGN>(S[i - 1][k])) -
+                               (ext32<SGN>(S[i - 1][k]) - ext32<SGN>(S[i - 2][k]));
+            const uint32_t code = (dd < 0 ? 1u << bitsize : 0u) | (uint32_t)uabs(dd);
+            const uint32_t bp = (P - 2) * cb, c = bp >> 5, o = bp & 31;
+            const uint32_t e = o + cb;  // <= 63
+            const uint32_t hi = e <= 32 ? code << (32 - e) : code >> (e - 32);
+            atomicOr(&L.B[WD0 + (c ^ 1)], hi);
+            if (e > 32) atomicOr(&L.B[WD0 + ((c + 1) ^ 1)], code << (64 - e));
+          }
+      }
+      __syncthreads();  // B2: DD output complete
+      // ---- BWR windows: 16 lanes each, 32 per pass; elements into registers ----
+      const uint32_t nw = (Ld + 255) / 256;
+      const uint32_t g = T >> 4, li = T & 15;
+      uint32_t E[PASSES][4];
+#pragma unroll
+      for (uint32_t p = 0; p < PASSES; p++) {
+        const uint32_t wi = 32 * p + g;
+        E[p][0] = E[p][1] = E[p][2] = E[p][3] = 0;
+        if (32 * p < nw) {  // (uniform)
+          if (wi < nw) {  // (uniform over the window's 16 lanes)
+            // DD-output bytes [256 wi + 16 li, +16) = LDS dwords from 592 + 64 wi + 4 li, shifted by 2
+            const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 4 * li;
+            const v4u q = *(const v4u*)(L.B + d0);
+            const uint32_t q4 = L.B[d0 + 4];
+            E[p][0] = __builtin_amdgcn_alignbyte(q.y, q.x, 2);
+            E[p][1] = __builtin_amdgcn_alignbyte(q.z, q.y, 2);
+            E[p][2] = __builtin_amdgcn_alignbyte(q.w, q.z, 2);
+            E[p][3] = __builtin_amdgcn_alignbyte(q4, q.w, 2);
+            const uint32_t nb = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
+            const uint32_t ne = nb >> 2;
+            int64_t mn = SGN ? INT64_MAX : (int64_t)UINT32_MAX, mxv = SGN ? INT64_MIN : 0;
+            bool have = false;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              if (4 * li + e < ne) {
+                const int64_t v = ext32<SGN>(E[p][e]);
+                mn = v < mn ? v : mn;
+                mxv = v > mxv ? v : mxv;
+                have = true;
+              }
+            }
+            grp_minmax<SGN>(mn, mxv);
+            (void)have;
+            if (li == 0) {
+              // compute_bits_required (bit_width_reduction_filter.cc:406-447)
+              uint32_t bits = 32;
+              int32_t minv = 0;
+              if (ne > 0) {
+                if (SGN) {
+                  const int64_t range = mxv - mn;
+                  if (!(range > 2147483647LL || range + 1 > 2147483647LL)) {
+                    const int64_t ro = range + 1;
+                    bits = ro <= 127 ? 8 : ro <= 32767 ? 16 : 32;
+                    minv = (int32_t)mn;
+                  }
+                } else {
+                  const uint64_t range = (uint64_t)mxv - (uint64_t)mn;
+                  if (range != 0xffffffffull) {
+                    const uint64_t ro = range + 1;
+                    const uint32_t nbits = 64 - __builtin_clzll(ro);
+                    bits = nbits <= 8 ? 8 : nbits <= 16 ? 16 : 32;
+                    minv = (int32_t)(uint32_t)mn;
+                  }
+                }
+              }
+              const bool wraw = bits >= 32 || (nb & 3) != 0;
+              L.wcs[wi] = wraw ? nb : ne * (bits >> 3);
+              L.wkind[wi] = wraw ? 2u : bits == 8 ? 0u : 1u;
+              L.wmin[wi] = minv;
+              // md entry [i32 minv][u8 bits][u32 nb] at image MD + 8 + 9 wi
+              const uint32_t ml = 8 + 9 * nw + 24;
+              const uint32_t eo = X0 - ml + 8 + 9 * wi;
+              lds_u32b(L, eo, (uint32_t)minv);
+              lds_byte(L, eo + 4, bits);
+              lds_u32b(L, eo + 5, nb);
+            }
+          }
+        }
+      }
+      __syncthreads();  // B3: window table
+      // exclusive scan of the compressed sizes (thread = window)
+      const uint32_t cs = T < nw ? L.wcs[T] : 0u;
+      const uint32_t inc = wave_incscan_u32(cs);
+      if (l == 63) L.scan[w] = inc;
+      __syncthreads();  // B4
+      uint32_t pre = 0, fl = 0;
+#pragma unroll
+      for (int v = 0; v < NWV; v++) {
+        const uint32_t x = L.scan[v];
+        pre += (uint32_t)v < w ? x : 0u;
+        fl += x;
+      }
+      if (T < nw) L.wcs[T] = pre + inc - cs;  // (read only after B5)
+      const uint32_t ml = 8 + 9 * nw + 24;
+      const uint32_t S0 = X0 - ml - 20;
+      const uint32_t total = 20 + ml + fl;
+      ok = total <= cap;
+      if (T == 0) {
+        // tile header [u64 1][u32 65536][u32 fl][u32 ml], BWR md head
+        // [u32 Ld][u32 nw], compression frame [1][1][8][17][65536][cl1]
+        lds_u32b(L, S0, 1);
+        lds_u32b(L, S0 + 4, 0);
+        lds_u32b(L, S0 + 8, TB);
+        lds_u32b(L, S0 + 12, fl);
+        lds_u32b(L, S0 + 16, ml);
+        lds_u32b(L, S0 + 20, Ld);
+        lds_u32b(L, S0 + 24, nw);
+        const uint32_t fo = S0 + 28 + 9 * nw;
+        lds_u32b(L, fo, 1);
+        lds_u32b(L, fo + 4, 1);
+        lds_u32b(L, fo + 8, 8);
+        lds_u32b(L, fo + 12, 17);
+        lds_u32b(L, fo + 16, TB);
+        lds_u32b(L, fo + 20, cl1);
+      }
+      __syncthreads();  // B5: offsets; every element is in registers
+      // ---- compressed windows, in place below the DD output ----
+#pragma unroll
+      for (uint32_t p = 0; p < PASSES; p++) {
+        const uint32_t wi = 32 * p + g;
+        if (32 * p < nw && wi < nw) {
+          const uint32_t off = L.wcs[wi], kind = L.wkind[wi];
+          const uint32_t mnv = (uint32_t)L.wmin[wi];
+          const uint32_t a = X0 + off;  // 4-aligned: every earlier window's size is a multiple of 4
+          if (kind == 0) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) x |= ((E[p][e] - mnv) & 0xffu) << (8 * e);
+            L.B[(a >> 2) + li] = x;
+          } else if (kind == 1) {
+            const uint32_t x0 = ((E[p][0] - mnv) & 0xffffu) | ((E[p][1] - mnv) << 16);
+            const uint32_t x1 = ((E[p][2] - mnv) & 0xffffu) | ((E[p][3] - mnv) << 16);
+            *(uint2*)(L.B + (a >> 2) + 2 * li) = make_uint2(x0, x1);
+          } else {
+            *(v4u*)(L.B + (a >> 2) + 4 * li) = v4u{E[p][0], E[p][1], E[p][2], E[p][3]};
+          }
+        }
+      }
+      __syncthreads();  // B6: the filtered image is complete in LDS
+      if (ok) {
+        // ---- store: image bytes [S0, S0 + total) to out, 16-B lane units ----
+        const uint32_t s3 = S0 & 3, sd = S0 >> 2;
+        const uint32_t nu = (total + 15) >> 4;
+        for (uint32_t u = T; u < nu; u += NT) {
+          const uint32_t* p = L.B + sd + 4 * u;
+          const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+          const v4u y{__builtin_amdgcn_alignbyte(d1, d0, s3), __builtin_amdgcn_alignbyte(d2, d1, s3),
+                      __builtin_amdgcn_alignbyte(d3, d2, s3), __builtin_amdgcn_alignbyte(d4, d3, s3)};
+          if (16 * u + 16 <= total) {
+            __builtin_nontemporal_store(y, (g_u4*)(out + 16 * u));
+          } else {
+            const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
+            for (uint32_t b = 0; 16 * u + b < total; b++) out[16 * u + b] = (uint8_t)(yy[b >> 2] >> (8 * (b & 3)));
+          }
+        }
+        if (T == 0) {
+          if (kp.stats) atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FWD_STREAM_TILES], 1ull);
+          if (kp.status) kp.status[t] = TDBG_OK;
+          if (kp.need) kp.need[t] = 0;
+          if (kp.out_len) kp.out_len[t] = total;
+        }
+      }
+    }
+    if (!ok && T == 0) {
+      // the general forward kernel takes this tile (and reports OUT_FULL etc.)
+      const uint32_t k = atomicAdd(kp.fbq, 1u);
+      if (k < kp.fbq_cap) kp.fbq[1 + k] = (uint32_t)t;
+      else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
+    }
+  }
+}
+
+}  // namespace fws
+}  // namespace tdbg
+
+// sgn: the DD and BWR stages' integer type (INT32 / UINT32) is signed
+extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
+  using namespace tdbg::fws;
+  if (sgn) hipLaunchKernelGGL((filter_stream_c5_kernel<true>), dim3(grid), dim3(NT), 0, s, *kp);
+  else hipLaunchKernelGGL((filter_stream_c5_kernel<false>), dim3(grid), dim3(NT), 0, s, *kp);
+  return hipGetLastError();
+}

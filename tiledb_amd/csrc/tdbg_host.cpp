@@ -28,6 +28,7 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
 extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
+extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
                                             tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
                                             uint64_t* need, hipStream_t stream);
@@ -54,6 +55,9 @@ extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid,
 extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
+extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
+                                               hipStream_t s);
+extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
 extern "C" hipError_t tdbg_launch_dense_copy(const tdbg_dense_copy_config* cfg, uint64_t ntiles,
                                              const int64_t* tile_start, const uint8_t* const* tiles,
                                              const int32_t* status, uint8_t* result, uint32_t grid,
@@ -643,9 +647,18 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
   static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
-  const bool streamed = queued && !chunked && !d_list && !no_stream &&
-                        (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
-                        p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
+  const bool c5_stream = (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
+                         p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
+  // The scan pipelines of C3a / C3b / C4 on 8-byte values first go through
+  // the small-image streaming kernel (tdbg_stream_small.hip): 0 [DD],
+  // 1 [RLE] with 8-byte cells, 2 [PD, BWR]; -1 none.
+  const tdbg_plan& P = p->plan;
+  const int small_mode = (P.fast == 12 && P.nstages == 1 && P.s[0].w == 8)                     ? 0
+                         : (P.fast == 14 && P.nstages == 1 && P.s[0].cs == 8)                  ? 1
+                         : ((P.fast == 15 || P.fast == 16) && P.nstages == 2 && P.s[0].w == 8 &&
+                            P.s[0].dts == 8 && P.s[1].w == 8 && P.s[1].dts == 8)               ? 2
+                                                                                               : -1;
+  const bool streamed = queued && !chunked && !d_list && !no_stream && (c5_stream || small_mode >= 0);
   // The fallback queue starts empty for this launch, whatever ran before on
   // any stream: a memset, or in a streamed launch the streaming kernel's first
   // thread (it runs before the fused kernel that appends).  The streaming
@@ -708,11 +721,18 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     ks.sq_cap = (uint32_t)ntiles;
     // the coded-DD kernel takes the tiles of at most its staging cap, the
     // raw-DD kernel the bigger ones; both queue what they decline
-    const int sgn = p->plan.s[2].sgn ? 1 : 0;
-    if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
-    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
-    if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
-    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
+    if (small_mode >= 0) {
+      const int sgn = (small_mode == 2 && P.s[1].sgn) ? 1 : 0;
+      if (!skip_fused)
+        e = tdbg_launch_stream_small(&ks, tdbg_stream_small_grid(c->cus, small_mode), small_mode, sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
+    } else {
+      const int sgn = p->plan.s[2].sgn ? 1 : 0;
+      if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+      if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
+    }
     tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
     kf.tile_list = c->d_sq + 1;
     kf.ntiles_dev = c->d_sq;
@@ -949,7 +969,30 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
   kp.slot_cap = slot_cap;
   kp.md_cap = md_cap;
   kp.tab_cap = tab_cap;
-  hipError_t e = tdbg_launch_filter(&kp, grid, s);
+  // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR(256)] on INT32 /
+  // UINT32 with one 64 KiB chunk per 64 KiB tile first goes through the
+  // LDS-resident forward kernel (tdbg_forward_stream.hip); the tiles it does
+  // not take (other sizes, alignments, capacities) are queued in the fused
+  // fallback queue for the general forward kernel, which runs on the queue.
+  static const bool no_fast = getenv("TDBG_NO_FWD_STREAM") != nullptr;  // ablation
+  const tdbg_plan& P = p->plan;
+  const bool c5 = !no_fast && !d_list && (P.fast == 19 || P.fast == 20) && P.nstages == 3 && P.s[0].w == 4 &&
+                  P.s[1].w == 4 && P.s[2].w == 4 && P.s[2].dts == 4 && P.s[1].sgn == P.s[2].sgn &&
+                  P.s[2].window == 256 && p->cell_size == 4 && (max_chunk == 0 || max_chunk >= 65536) &&
+                  n <= c->status_cap;
+  hipError_t e = hipSuccess;
+  if (c5) {
+    HIP_OK(hipMemsetAsync(c->d_fbq, 0, sizeof(uint32_t), s));
+    tdbg::KParams kf = kp;
+    kf.fbq = c->d_fbq;
+    kf.fbq_cap = (uint32_t)n;
+    kf.stats = c->d_stats;
+    e = tdbg_launch_filter_c5(&kf, (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2), P.s[2].sgn ? 1 : 0, s);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward stream launch: ") + hipGetErrorString(e));
+    kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
+    kp.ntiles_dev = c->d_fbq;
+  }
+  e = tdbg_launch_filter(&kp, grid, s);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("filter launch: ") + hipGetErrorString(e));
   return TDBG_OK;
 }
@@ -1090,6 +1133,15 @@ int tdbg_context_stream_stats(const tdbg_context* c, uint64_t* stream_tiles) {
   int rc = read_stats(c, h);
   if (rc) return rc;
   if (stream_tiles) *stream_tiles = h[TDBG_STAT_STREAM_TILES];
+  return TDBG_OK;
+}
+
+int tdbg_context_forward_stream_stats(const tdbg_context* c, uint64_t* tiles) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (tiles) *tiles = h[TDBG_STAT_FWD_STREAM_TILES];
   return TDBG_OK;
 }
 

@@ -290,6 +290,12 @@ class Context:
         _check(lib.tdbg_context_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_stats")
         return int(n.value)
 
+    def forward_stream_tiles(self):
+        """Tiles the LDS-resident C5 forward kernel filtered, cumulative (synchronizes)."""
+        n = ctypes.c_uint64()
+        _check(lib.tdbg_context_forward_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_forward_stream_stats")
+        return int(n.value)
+
     def stream_raw_tiles(self):
         """Of those, the tiles the raw-DoubleDelta streaming kernel took, cumulative."""
         n = ctypes.c_uint64()
