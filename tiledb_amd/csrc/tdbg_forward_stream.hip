@@ -175,6 +175,12 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       mx = 0;
 #pragma unroll
       for (int v = 0; v < NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
+      // (the 64-bit extensions of the bit-size pass are recomputed below, not
+      // kept live across the barrier: 40 values would take 80 registers)
+#pragma unroll
+      for (int i = 0; i < 10; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) asm volatile("" : "+v"(S[i][k]));
       const uint32_t bitsize = mx ? 64 - __builtin_clzll(mx) : 1;  // do { ++b; m >>= 1; } while (m)
       const bool raw = bitsize >= 31;
       const uint32_t cb = bitsize + 1;
