@@ -151,9 +151,10 @@ def test_forward_stream_c5_kernel(eng, ctx, oracle_mod):
 
 
 def test_forward_stream_c5_declines(eng, ctx, oracle_mod):
-    """Tiles the C5 forward kernel does not take (not 64 KiB, another BWR
-    window, a different max chunk) run on the general forward kernel with
-    the oracle's bytes; a 64 KiB tile next to them is still taken."""
+    """Tiles the C5 forward kernel does not take (not 64 KiB, not 16-B
+    aligned in the packed input, another BWR window, a different max chunk)
+    run on the general forward kernel with the oracle's bytes; a 64 KiB tile
+    at an aligned start next to them is still taken."""
     import workloads as W
     from tests.cases import P, DD, Case
     from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
@@ -162,7 +163,9 @@ def test_forward_stream_c5_declines(eng, ctx, oracle_mod):
     odd = [full[:4000].copy(), full[:65532].copy(), np.concatenate([full, full[:400]])]
     pipe = P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(256))
     f0 = ctx.forward_stream_tiles()
-    forward_parity(eng, ctx, oracle_mod, Case("c5fs_odd", pipe, Datatype.INT32, 4, odd + [full]))
+    # (ctx.filter packs the inputs back to back: the last full tile starts
+    # 135,468 bytes in, not 16-B aligned)
+    forward_parity(eng, ctx, oracle_mod, Case("c5fs_odd", pipe, Datatype.INT32, 4, [full] + odd + [full]))
     assert ctx.forward_stream_tiles() - f0 == 1
     f0 = ctx.forward_stream_tiles()
     forward_parity(eng, ctx, oracle_mod, Case("c5fs_w512", P(ByteshuffleFilter(), DD(), BitWidthReductionFilter(512)),

@@ -1,5 +1,5 @@
 """Summary of tools/profile_all.sh: per (config, variant) the unfilter kernels'
-(streaming + fused on its queue for C5, else fused) rocprofv3 kernel-trace average over the timed launches, per-launch HBM
+(streaming kernels + fused on their queue for C3/C4/C5, else fused) rocprofv3 kernel-trace average over the timed launches, per-launch HBM
 traffic from the --pmc passes (KiB -> bytes; FETCH_SIZE doubled for gfx950
 16-B/lane streaming reads, MI355X_MICROARCH.md "HBM"), the algorithmic bytes
 and roofline fraction from the bench line of the same workload."""
@@ -13,21 +13,24 @@ import sys
 PEAK = 8000.0
 
 
-KERNELS = ("unfilter_stream_kernel", "unfilter_fused_kernel")
+KERNELS = ("unfilter_stream", "unfilter_fused_kernel")
+STARTS = ("unfilter_stream_kernel", "unfilter_stream_small_kernel")
 
 
 def _launches(items):
     """items: (order key, kernel name, value) of the unfilter kernels.  A launch
-    is the streaming kernel plus the fused kernel on its queue (C5), or the
-    fused kernel alone; values of one launch are summed."""
+    is a streaming kernel (C5: coded then raw-DD; C3/C4: small-image) plus the
+    fused kernel on its queue, or the fused kernel alone; values of one launch
+    are summed."""
     out, open_stream = [], False
     for _, name, v in sorted(items):
-        if "unfilter_stream_kernel" in name:
+        if any(k in name for k in STARTS):
             out.append(v)
             open_stream = True
         elif open_stream:
             out[-1] += v
-            open_stream = False
+            if "unfilter_fused_kernel" in name:
+                open_stream = False
         else:
             out.append(v)
     return out
