@@ -533,7 +533,9 @@ def main():
         _, bres = run_config(engine, ctx, W, args, "c5", variants, args.big_tiles, max(3, args.steps // 4),
                              2, dist, world, rank)
         for v in variants:
-            big[v] = variant_line("c5big", v, bres[v], world)
+            # (no PMC pass of this 100k-tile workload is committed: traffic null,
+            # not the 12,500-tile or 4 MiB-tile figure)
+            big[v] = variant_line("c5_100k", v, bres[v], world)
             bres[v].pop("packed", None)
         line["config"]["c5_100k_single_gpu"] = {
             "tiles": args.big_tiles, "steps": max(3, args.steps // 4), "variants": big,
