@@ -320,6 +320,8 @@ def kernel_name(cfgname, r):
     if cfgname in ("c5", "c5big") and r["streamed"]:
         return ("unfilter_stream_kernel + unfilter_stream_raw_kernel + unfilter_fused_kernel (queue of "
                 "declined tiles)")
+    if cfgname == "c1" and r["streamed"]:
+        return "unfilter_shuffle4_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname in ("c3a", "c3b", "c4") and r["streamed"]:
         return "unfilter_stream_small_kernel + unfilter_fused_kernel (queue of declined tiles)"
     return "unfilter_fused_kernel"

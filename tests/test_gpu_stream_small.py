@@ -308,3 +308,62 @@ def test_small_wrong_sizes_and_offsets(eng, ctx, oracle_mod, cfg):
     check_parity(eng, ctx, oracle_mod, Case(f"{cfg}_sizes", pipe, dt, cs, []), tiles, sizes)
     case = Case(f"{cfg}_offs", pipe, dt, cs, [], offsets_tile=True)
     check_parity(eng, ctx, oracle_mod, case, tiles, [65536 + 8] * len(tiles))
+
+
+# ---------------------------------------------------------------------------
+# C1: [BYTESHUFFLE] on 4-byte values (tdbg_stream_shuffle.hip)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("align", [1, 16])
+@pytest.mark.parametrize("ntiles", [7, 256, 700])
+def test_shuffle4_config_tiles(eng, ctx, oracle_mod, ntiles, align):
+    """SURVEY's C1 tiles (ramp and rand), back to back or 16-B aligned, also
+    fewer tiles than CUs: every one taken by the unit-parallel kernel."""
+    from tests.test_gpu_parity import check_parity, encode
+    from tests.cases import c1_tiles
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter
+    tiles = c1_tiles(4, "ramp") + c1_tiles(4, "rand")
+    case = Case("c1", P(ByteshuffleFilter()), Datatype.INT32, 4, tiles)
+    _, enc = encode(oracle_mod, case)
+    enc = (enc * -(-ntiles // len(enc)))[:ntiles]
+    f0, b0, _ = ctx.path_stats()
+    s0 = ctx.stream_tiles()
+    check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc], [e[1] for e in enc],
+                 align=align)
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0 and f1 - f0 == ntiles
+    assert ctx.stream_tiles() - s0 == ntiles
+
+
+def test_shuffle4_declined_tiles(eng, ctx, oracle_mod):
+    """Other shapes (other sizes, two parts, UINT32 is taken, INT16 is not),
+    corrupted headers, wrong output sizes and offsets tiles get the oracle's
+    status and bytes."""
+    from tests.test_gpu_parity import check_parity, encode
+    from tests.cases import c1_tiles
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter
+    rng = np.random.default_rng(63)
+    pipe = P(ByteshuffleFilter())
+    base = c1_tiles(3, "rand")
+    odd = [base[0][:4000].copy(), base[1][:65532].copy()]
+    case = Case("c1_odd", pipe, Datatype.INT32, 4, base + odd)
+    _, enc = encode(oracle_mod, case)
+    tiles = [e[0] for e in enc]
+    sizes = [e[2] for e in enc]
+    for f in list(tiles[:3]):
+        for pos in (0, 4, 8, 12, 16, 20, 24, 28, f.size - 1):
+            g = f.copy()
+            g[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+            tiles.append(g)
+            sizes.append(65536)
+        tiles.append(f[: f.size - 1].copy())
+        sizes.append(65536)
+        tiles.append(f.copy())
+        sizes.append(65536 + 8)
+    rep = -(-320 // len(tiles))
+    check_parity(eng, ctx, oracle_mod, Case("c1_mix", pipe, Datatype.INT32, 4, []), tiles * rep, sizes * rep)
+    off = Case("c1_offs", pipe, Datatype.INT32, 4, [], offsets_tile=True)
+    check_parity(eng, ctx, oracle_mod, off, [e[0] for e in enc] * 64, [e[2] + 8 for e in enc] * 64)
+    i16 = Case("c1_i16", pipe, Datatype.INT16, 2, [t.copy() for t in base])
+    s0 = ctx.stream_tiles()
+    _run(eng, ctx, oracle_mod, i16)
+    assert ctx.stream_tiles() == s0

@@ -67,10 +67,39 @@ static_assert(DELTA % 4 == 2 && X0 >= 20 + MLMAX, "LDS image layout");
 struct Lds {
   uint32_t B[BDW];
   uint32_t wcs[NWMAX + 7];   // window compressed bytes, then (after the scan) its data offset
-  uint32_t wkind[NWMAX + 7]; // 0: 8-bit, 1: 16-bit, 2: raw
+  uint32_t wbits[NWMAX + 7]; // the window's bits field
   int32_t wmin[NWMAX + 7];
-  uint64_t red[NWV];
+  uint64_t red[4 * NWV];
   uint32_t scan[NWV];
+  uint64_t clk[8];  // diagnostics: phase clocks (TDBG_PROF)
+};
+
+// Diagnostics (KParams::prof, TDBG_PROF=1): per-workgroup shader-clock
+// cycles per phase: 0 loads + transposes (after B0), 1 bit size + B1, 2 DD
+// output + B2, 3 BWR window pass + B3, 4 scan + headers + B4/B5, 5 in-place
+// compression + B6, 6 image store
+struct Clock {
+  uint64_t* out;
+  uint64_t* acc;
+  uint64_t t;
+  __device__ __forceinline__ void init(uint64_t* o, uint64_t* a) {
+    out = o;
+    acc = a;
+    if (!out) return;
+    t = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 8; k++) acc[k] = 0;
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (!out) return;
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) acc[k] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void flush() {
+    if (!out || threadIdx.x != 0) return;
+    for (int k = 0; k < 8; k++) out[blockIdx.x * TDBG_PROF_PHASES + k] = acc[k];
+  }
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -101,20 +130,55 @@ __device__ __forceinline__ int64_t ext32(uint32_t v) {
 }
 __device__ __forceinline__ uint64_t uabs(int64_t v) { return v < 0 ? 0ull - (uint64_t)v : (uint64_t)v; }
 
-// 16-lane group reductions (lanes of one BWR window)
+// Reductions over a 16-lane DPP row (the lanes of one BWR window, or a
+// wave's row): quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
+// -- every lane ends with the row's result, VALU only.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
 template <bool SGN>
-__device__ __forceinline__ void grp_minmax(int64_t& mn, int64_t& mx) {
-#pragma unroll
-  for (int d = 8; d >= 1; d >>= 1) {
-    const int64_t a = __shfl_xor(mn, d, 16), b = __shfl_xor(mx, d, 16);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
+__device__ __forceinline__ void row_minmax(uint32_t& mn, uint32_t& mx) {
+  auto step = [&](uint32_t a, uint32_t b) {
+    if (SGN) {
+      mn = (int32_t)a < (int32_t)mn ? a : mn;
+      mx = (int32_t)b > (int32_t)mx ? b : mx;
+    } else {
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+  };
+  step(dpp_<0xB1>(mn), dpp_<0xB1>(mx));
+  step(dpp_<0x4E>(mn), dpp_<0x4E>(mx));
+  step(dpp_<0x141>(mn), dpp_<0x141>(mx));
+  step(dpp_<0x140>(mn), dpp_<0x140>(mx));
+}
+__device__ __forceinline__ uint64_t row_max64(uint64_t v) {
+  auto step = [&](uint64_t o) { v = o > v ? o : v; };
+  step(((uint64_t)dpp_<0xB1>((uint32_t)(v >> 32)) << 32) | dpp_<0xB1>((uint32_t)v));
+  step(((uint64_t)dpp_<0x4E>((uint32_t)(v >> 32)) << 32) | dpp_<0x4E>((uint32_t)v));
+  step(((uint64_t)dpp_<0x141>((uint32_t)(v >> 32)) << 32) | dpp_<0x141>((uint32_t)v));
+  step(((uint64_t)dpp_<0x140>((uint32_t)(v >> 32)) << 32) | dpp_<0x140>((uint32_t)v));
+  return v;
 }
 
 template <bool SGN>
 __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams kp) {
   __shared__ Lds L;
+  Clock pc;
+  pc.init(kp.prof, L.clk);
+  auto shape_of = [&](uint64_t jj) {
+    const uint8_t* ii = kp.in[jj];
+    return kp.in_size[jj] == TB && (((uintptr_t)ii) & 15) == 0 && (((uintptr_t)kp.out[jj]) & 15) == 0 &&
+           kp.out_size[jj] >= 64;
+  };
+  v4u U[10];
+  auto load_units = [&](uint64_t jj, uint32_t T) {
+    // units 8T..8T+7 and the two before (wrapping into the last plane's end for T = 0)
+    const g_cu4* src = (const g_cu4*)kp.in[jj];
+#pragma unroll
+    for (int i = 0; i < 10; i++) U[i] = src[(8 * T + i - 2) & 4095u];
+  };
   for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
     // thread index opaque to the optimizer: the unrolled per-thread index
     // math is tile-invariant, and hoisting it out of the tile loop pins (and
@@ -123,23 +187,20 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
     asm volatile("" : "+v"(T));
     const uint32_t l = T & 63, w = __builtin_amdgcn_readfirstlane(T >> 6);
     const uint64_t t = j;
-    const uint8_t* in = kp.in[t];
     uint8_t* out = kp.out[t];
-    const uint64_t isz = kp.in_size[t], cap = kp.out_size[t];
+    const uint64_t cap = kp.out_size[t];
     // this kernel's tile shape; anything else goes to the general kernel
-    const bool shape = isz == TB && (((uintptr_t)in) & 15) == 0 && (((uintptr_t)out) & 15) == 0 && cap >= 64;
+    const bool shape = shape_of(t);
     bool ok = shape;
     __syncthreads();  // B0: the last tile's image is stored (LDS free)
     if (shape) {
+      // (issued first: their latency overlaps the zeroing below; a prefetch
+      // one tile ahead, issued before the last tile's image store, measured
+      // slower: the store phase waited behind the loads)
+      load_units(t, T);
       // ---- zero the DD word region (codes are OR-ed in) ----
       static_assert(BDW % 4 == 0, "16-B zeroing");
       for (uint32_t d = (WD0 & ~3u) + 4 * T; d < BDW; d += 4 * NT) *(v4u*)(L.B + d) = v4u{0u, 0u, 0u, 0u};
-      // ---- loads: units 8T..8T+7 and the two before (wrapping into the last
-      // plane's end for T = 0) ----
-      const g_cu4* src = (const g_cu4*)in;
-      v4u U[10];
-#pragma unroll
-      for (int i = 0; i < 10; i++) U[i] = src[(8 * T + i - 2) & 4095u];
       // S[i][k]: position 8T + i - 2 of plane k (for T = 0 and i < 2: plane k-1's end)
       uint32_t S[10][4];
 #pragma unroll
@@ -153,6 +214,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           S[i][0] = 0;  // (positions -2, -1 do not exist)
         }
       }
+      pc.mark(0);
       // ---- DoubleDelta bit size: max(|d1|, |dd_i|), i >= 2 ----
       uint64_t mx = 0;
 #pragma unroll
@@ -165,16 +227,12 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           const uint64_t a = P >= 2 ? uabs(d - dp) : P == 1 ? uabs(d) : 0ull;
           mx = a > mx ? a : mx;
         }
-#pragma unroll
-      for (int dd = 32; dd >= 1; dd >>= 1) {
-        const uint64_t y = __shfl_xor(mx, dd, 64);
-        mx = y > mx ? y : mx;
-      }
-      if (l == 0) L.red[w] = mx;
+      mx = row_max64(mx);
+      if ((l & 15) == 0) L.red[4 * w + (l >> 4)] = mx;
       __syncthreads();  // B1
       mx = 0;
 #pragma unroll
-      for (int v = 0; v < NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
+      for (int v = 0; v < 4 * NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
       // (the 64-bit extensions of the bit-size pass are recomputed below, not
       // kept live across the barrier: 40 values would take 80 registers)
 #pragma unroll
@@ -182,6 +240,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
 #pragma unroll
         for (int k = 0; k < 4; k++) asm volatile("" : "+v"(S[i][k]));
       const uint32_t bitsize = mx ? 64 - __builtin_clzll(mx) : 1;  // do { ++b; m >>= 1; } while (m)
+      pc.mark(1);
       const bool raw = bitsize >= 31;
       const uint32_t cb = bitsize + 1;
       const uint32_t words = raw ? 0u : ((NV - 2) * cb + 63) / 64;
@@ -211,23 +270,42 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           L.B[(DELTA + 26) / 4] = S[2][0];
           L.B[(DELTA + 30) / 4] = S[3][0];
         }
+        // A run (plane k) is 8 consecutive codes = one contiguous bit range:
+        // its codes are shifted into a 64-bit accumulator and every whole
+        // 32-bit chunk leaves as it fills -- plain stores for the chunks the
+        // run owns, ds_or only for its first and last chunk (shared with the
+        // neighbouring runs; the region was zeroed before B1).
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < 4; k++) {
+          const uint32_t P0 = 4096 * k + 8 * T;
+          const uint32_t i0 = P0 < 2 ? 2 + (2 - P0) : 2;  // (T = 0, k = 0: codes from position 2)
+          const uint32_t bp0 = ((P0 < 2 ? 2 : P0) - 2) * cb;
+          uint32_t c = bp0 >> 5, nb = bp0 & 31;  // chunk being filled, bits already in it
+          uint64_t acc = 0;
+          bool first = true;
 #pragma unroll
           for (int i = 2; i < 10; i++) {
-            const uint32_t P = 4096 * k + 8 * T + i - 2;
-            if (P < 2) continue;
-            const int64_t dd = (ext32<SGN>(S[i][k]) - ext32<SGN>(S[i - 1][k])) -
-                               (ext32<SGN>(S[i - 1][k]) - ext32<SGN>(S[i - 2][k]));
-            const uint32_t code = (dd < 0 ? 1u << bitsize : 0u) | (uint32_t)uabs(dd);
-            const uint32_t bp = (P - 2) * cb, c = bp >> 5, o = bp & 31;
-            const uint32_t e = o + cb;  // <= 63
-            const uint32_t hi = e <= 32 ? code << (32 - e) : code >> (e - 32);
-            atomicOr(&L.B[WD0 + (c ^ 1)], hi);
-            if (e > 32) atomicOr(&L.B[WD0 + ((c + 1) ^ 1)], code << (64 - e));
+            if ((uint32_t)i < i0) continue;
+            // (coded: |dd| < 2^30, so the wrapped 32-bit value is exact)
+            const int32_t dd = (int32_t)(S[i][k] - 2u * S[i - 1][k] + S[i - 2][k]);
+            const uint32_t code = (dd < 0 ? 1u << bitsize : 0u) | (uint32_t)(dd < 0 ? -dd : dd);
+            acc = (acc << cb) | code;  // low nb + cb <= 63 bits pending
+            nb += cb;
+            if (nb >= 32) {
+              const uint32_t chunk = (uint32_t)(acc >> (nb - 32));
+              if (first) atomicOr(&L.B[WD0 + (c ^ 1)], chunk);
+              else L.B[WD0 + (c ^ 1)] = chunk;
+              first = false;
+              c++;
+              nb -= 32;
+              acc &= (1ull << nb) - 1;
+            }
           }
+          if (nb) atomicOr(&L.B[WD0 + (c ^ 1)], (uint32_t)(acc << (32 - nb)));
+        }
       }
       __syncthreads();  // B2: DD output complete
+      pc.mark(2);
       // ---- BWR windows: 16 lanes each, 32 per pass; elements into registers ----
       const uint32_t nw = (Ld + 255) / 256;
       const uint32_t g = T >> 4, li = T & 15;
@@ -248,19 +326,22 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
             E[p][3] = __builtin_amdgcn_alignbyte(q4, q.w, 2);
             const uint32_t nb = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
             const uint32_t ne = nb >> 2;
-            int64_t mn = SGN ? INT64_MAX : (int64_t)UINT32_MAX, mxv = SGN ? INT64_MIN : 0;
-            bool have = false;
+            uint32_t mn32 = SGN ? 0x7fffffffu : 0xffffffffu, mx32 = SGN ? 0x80000000u : 0u;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
               if (4 * li + e < ne) {
-                const int64_t v = ext32<SGN>(E[p][e]);
-                mn = v < mn ? v : mn;
-                mxv = v > mxv ? v : mxv;
-                have = true;
+                const uint32_t v = E[p][e];
+                if (SGN) {
+                  mn32 = (int32_t)v < (int32_t)mn32 ? v : mn32;
+                  mx32 = (int32_t)v > (int32_t)mx32 ? v : mx32;
+                } else {
+                  mn32 = v < mn32 ? v : mn32;
+                  mx32 = v > mx32 ? v : mx32;
+                }
               }
             }
-            grp_minmax<SGN>(mn, mxv);
-            (void)have;
+            row_minmax<SGN>(mn32, mx32);
+            const int64_t mn = ext32<SGN>(mn32), mxv = ext32<SGN>(mx32);
             if (li == 0) {
               // compute_bits_required (bit_width_reduction_filter.cc:406-447)
               uint32_t bits = 32;
@@ -285,19 +366,14 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
               }
               const bool wraw = bits >= 32 || (nb & 3) != 0;
               L.wcs[wi] = wraw ? nb : ne * (bits >> 3);
-              L.wkind[wi] = wraw ? 2u : bits == 8 ? 0u : 1u;
+              L.wbits[wi] = bits;
               L.wmin[wi] = minv;
-              // md entry [i32 minv][u8 bits][u32 nb] at image MD + 8 + 9 wi
-              const uint32_t ml = 8 + 9 * nw + 24;
-              const uint32_t eo = X0 - ml + 8 + 9 * wi;
-              lds_u32b(L, eo, (uint32_t)minv);
-              lds_byte(L, eo + 4, bits);
-              lds_u32b(L, eo + 5, nb);
             }
           }
         }
       }
       __syncthreads();  // B3: window table
+      pc.mark(3);
       // exclusive scan of the compressed sizes (thread = window)
       const uint32_t cs = T < nw ? L.wcs[T] : 0u;
       const uint32_t inc = wave_incscan_u32(cs);
@@ -310,8 +386,17 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         pre += (uint32_t)v < w ? x : 0u;
         fl += x;
       }
-      if (T < nw) L.wcs[T] = pre + inc - cs;  // (read only after B5)
       const uint32_t ml = 8 + 9 * nw + 24;
+      if (T < nw) {
+        L.wcs[T] = pre + inc - cs;  // (read only after B5)
+        // md entry [i32 minv][u8 bits][u32 nb] at image MD + 8 + 9 T, one
+        // thread per window
+        const uint32_t nb = Ld - 256 * T < 256 ? Ld - 256 * T : 256;
+        const uint32_t eo = X0 - ml + 8 + 9 * T;
+        lds_u32b(L, eo, (uint32_t)L.wmin[T]);
+        lds_byte(L, eo + 4, L.wbits[T]);
+        lds_u32b(L, eo + 5, nb);
+      }
       const uint32_t S0 = X0 - ml - 20;
       const uint32_t total = 20 + ml + fl;
       ok = total <= cap;
@@ -334,12 +419,15 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         lds_u32b(L, fo + 20, cl1);
       }
       __syncthreads();  // B5: offsets; every element is in registers
+      pc.mark(4);
       // ---- compressed windows, in place below the DD output ----
 #pragma unroll
       for (uint32_t p = 0; p < PASSES; p++) {
         const uint32_t wi = 32 * p + g;
         if (32 * p < nw && wi < nw) {
-          const uint32_t off = L.wcs[wi], kind = L.wkind[wi];
+          const uint32_t off = L.wcs[wi], bits = L.wbits[wi];
+          const uint32_t nbw = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
+          const uint32_t kind = (bits >= 32 || (nbw & 3) != 0) ? 2u : bits == 8 ? 0u : 1u;
           const uint32_t mnv = (uint32_t)L.wmin[wi];
           const uint32_t a = X0 + off;  // 4-aligned: every earlier window's size is a multiple of 4
           if (kind == 0) {
@@ -357,6 +445,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         }
       }
       __syncthreads();  // B6: the filtered image is complete in LDS
+      pc.mark(5);
       if (ok) {
         // ---- store: image bytes [S0, S0 + total) to out, 16-B lane units ----
         const uint32_t s3 = S0 & 3, sd = S0 >> 2;
@@ -381,6 +470,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         }
       }
     }
+    pc.mark(6);
     if (!ok && T == 0) {
       // the general forward kernel takes this tile (and reports OUT_FULL etc.)
       const uint32_t k = atomicAdd(kp.fbq, 1u);
@@ -388,6 +478,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
     }
   }
+  pc.flush();
 }
 
 }  // namespace fws

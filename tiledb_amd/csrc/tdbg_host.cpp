@@ -58,6 +58,7 @@ extern "C" uint32_t tdbg_stream_raw_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                hipStream_t s);
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
+extern "C" hipError_t tdbg_launch_stream_shuffle4(const tdbg::KParams* kp, hipStream_t s);
 extern "C" hipError_t tdbg_launch_dense_copy(const tdbg_dense_copy_config* cfg, uint64_t ntiles,
                                              const int64_t* tile_start, const uint8_t* const* tiles,
                                              const int32_t* status, uint8_t* result, uint32_t grid,
@@ -641,8 +642,11 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
   static const bool tile_mode = getenv("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
+  // [BYTESHUFFLE] on 4-byte values (C1): the unit-parallel streaming kernel
+  // (tdbg_stream_shuffle.hip) splits every tile over 16 workgroups itself
+  const bool shuffle4 = p->plan.fast == 1 && p->plan.nstages == 1 && p->plan.s[0].w == 4;
   const bool chunked = queued && !d_list &&
-                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
+                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && !shuffle4 && ntiles < (uint64_t)c->cus));
   // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
@@ -658,7 +662,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
                          : ((P.fast == 15 || P.fast == 16) && P.nstages == 2 && P.s[0].w == 8 &&
                             P.s[0].dts == 8 && P.s[1].w == 8 && P.s[1].dts == 8)               ? 2
                                                                                                : -1;
-  const bool streamed = queued && !chunked && !d_list && !no_stream && (c5_stream || small_mode >= 0);
+  const bool streamed = queued && !chunked && !d_list && !no_stream && (c5_stream || small_mode >= 0 || shuffle4);
   // The fallback queue starts empty for this launch, whatever ran before on
   // any stream: a memset, or in a streamed launch the streaming kernel's first
   // thread (it runs before the fused kernel that appends).  The streaming
@@ -721,7 +725,10 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     ks.sq_cap = (uint32_t)ntiles;
     // the coded-DD kernel takes the tiles of at most its staging cap, the
     // raw-DD kernel the bigger ones; both queue what they decline
-    if (small_mode >= 0) {
+    if (shuffle4) {
+      if (!skip_fused) e = tdbg_launch_stream_shuffle4(&ks, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("shuffle stream kernel launch: ") + hipGetErrorString(e));
+    } else if (small_mode >= 0) {
       const int sgn = (small_mode == 2 && P.s[1].sgn) ? 1 : 0;
       if (!skip_fused)
         e = tdbg_launch_stream_small(&ks, tdbg_stream_small_grid(c->cus, small_mode), small_mode, sgn, stream);
@@ -987,7 +994,20 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kf.fbq = c->d_fbq;
     kf.fbq_cap = (uint32_t)n;
     kf.stats = c->d_stats;
-    e = tdbg_launch_filter_c5(&kf, (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2), P.s[2].sgn ? 1 : 0, s);
+    static const bool prof = getenv("TDBG_PROF") != nullptr;  // diagnostics: phase clocks
+    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
+    if (prof) {
+      if (c->prof_grid < fgrid) {
+        if (c->d_prof) (void)hipFree(c->d_prof);
+        c->d_prof = nullptr;
+        c->prof_grid = 0;
+        HIP_OK(hipMalloc(&c->d_prof, sizeof(uint64_t) * TDBG_PROF_PHASES * fgrid));
+        c->prof_grid = fgrid;
+      }
+      HIP_OK(hipMemsetAsync(c->d_prof, 0, sizeof(uint64_t) * TDBG_PROF_PHASES * c->prof_grid, s));
+      kf.prof = c->d_prof;
+    }
+    e = tdbg_launch_filter_c5(&kf, fgrid, P.s[2].sgn ? 1 : 0, s);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward stream launch: ") + hipGetErrorString(e));
     kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
     kp.ntiles_dev = c->d_fbq;
