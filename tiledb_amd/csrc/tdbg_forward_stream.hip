@@ -21,7 +21,7 @@
 //     stored raw (bitsize >= 31).  The compression filter's metadata part
 //     (the byteshuffle header: two int32) becomes the 17-byte DD part before
 //     it (compression_filter.cc:240-301).
-//   * BWR (bit_width_reduction_filter.cc:110-280, 406-447): 16 lanes per
+//   * BWR (bit_width_reduction_filter.cc:110-280, 406-447): 8 lanes per
 //     256-B window read its 64 elements once into registers; min / max give
 //     the window's width; an exclusive workgroup scan of the compressed
 //     sizes places every window; the compressed bytes are written in place
@@ -61,7 +61,8 @@ constexpr uint32_t X0 = DELTA - 2;          // compressed data byte 0
 constexpr uint32_t DOUT_MAX = 17 + 9 + TB;  // DD output bytes (raw)
 constexpr uint32_t BDW = (DELTA + DOUT_MAX + 320 + 15) / 16 * 4;  // image dwords (+ reads past the last window)
 constexpr uint32_t WD0 = (DELTA + 34) / 4;  // LDS dword of DD word 0
-constexpr uint32_t PASSES = (NWMAX + NT / 16 - 1) / (NT / 16);  // BWR window passes (9)
+constexpr uint32_t WPP = NT / 8;                          // BWR windows per pass (8 lanes each)
+constexpr uint32_t PASSES = (NWMAX + WPP - 1) / WPP;        // BWR window passes (5)
 static_assert(DELTA % 4 == 2 && X0 >= 20 + MLMAX, "LDS image layout");
 
 struct Lds {
@@ -138,7 +139,7 @@ __device__ __forceinline__ uint32_t dpp_(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
 template <bool SGN>
-__device__ __forceinline__ void row_minmax(uint32_t& mn, uint32_t& mx) {
+__device__ __forceinline__ void half_minmax(uint32_t& mn, uint32_t& mx) {  // over 8 lanes
   auto step = [&](uint32_t a, uint32_t b) {
     if (SGN) {
       mn = (int32_t)a < (int32_t)mn ? a : mn;
@@ -151,7 +152,6 @@ __device__ __forceinline__ void row_minmax(uint32_t& mn, uint32_t& mx) {
   step(dpp_<0xB1>(mn), dpp_<0xB1>(mx));
   step(dpp_<0x4E>(mn), dpp_<0x4E>(mx));
   step(dpp_<0x141>(mn), dpp_<0x141>(mx));
-  step(dpp_<0x140>(mn), dpp_<0x140>(mx));
 }
 __device__ __forceinline__ uint64_t row_max64(uint64_t v) {
   auto step = [&](uint64_t o) { v = o > v ? o : v; };
@@ -216,17 +216,27 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       }
       pc.mark(0);
       // ---- DoubleDelta bit size: max(|d1|, |dd_i|), i >= 2 ----
-      uint64_t mx = 0;
+      // (in f64, which holds every int32 / uint32 value and their first and
+      // second differences, |dd| < 2^34, exactly: one conversion, two
+      // subtractions and a max with an |.| modifier per value instead of
+      // 64-bit integer arithmetic)
+      double mxd = 0.0;
 #pragma unroll
-      for (int k = 0; k < 4; k++)
+      for (int k = 0; k < 4; k++) {
+        auto f = [&](uint32_t v) { return SGN ? (double)(int32_t)v : (double)v; };
+        double x2 = f(S[0][k]), x1 = f(S[1][k]);
 #pragma unroll
         for (int i = 2; i < 10; i++) {
           const uint32_t P = 4096 * k + 8 * T + i - 2;
-          const int64_t d = ext32<SGN>(S[i][k]) - ext32<SGN>(S[i - 1][k]);
-          const int64_t dp = ext32<SGN>(S[i - 1][k]) - ext32<SGN>(S[i - 2][k]);
-          const uint64_t a = P >= 2 ? uabs(d - dp) : P == 1 ? uabs(d) : 0ull;
-          mx = a > mx ? a : mx;
+          const double x = f(S[i][k]);
+          const double d = x - x1, dp = x1 - x2;
+          const double a = P >= 2 ? __builtin_fabs(d - dp) : P == 1 ? __builtin_fabs(d) : 0.0;
+          mxd = __builtin_fmax(mxd, a);
+          x2 = x1;
+          x1 = x;
         }
+      }
+      uint64_t mx = (uint64_t)mxd;
       mx = row_max64(mx);
       if ((l & 15) == 0) L.red[4 * w + (l >> 4)] = mx;
       __syncthreads();  // B1
@@ -306,30 +316,31 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       }
       __syncthreads();  // B2: DD output complete
       pc.mark(2);
-      // ---- BWR windows: 16 lanes each, 32 per pass; elements into registers ----
+      // ---- BWR windows: 8 lanes each (32 bytes a lane), 64 per pass; elements
+      // into registers ----
       const uint32_t nw = (Ld + 255) / 256;
-      const uint32_t g = T >> 4, li = T & 15;
-      uint32_t E[PASSES][4];
+      const uint32_t g = T >> 3, li = T & 7;
+      uint32_t E[PASSES][8];
 #pragma unroll
       for (uint32_t p = 0; p < PASSES; p++) {
-        const uint32_t wi = 32 * p + g;
-        E[p][0] = E[p][1] = E[p][2] = E[p][3] = 0;
-        if (32 * p < nw) {  // (uniform)
-          if (wi < nw) {  // (uniform over the window's 16 lanes)
-            // DD-output bytes [256 wi + 16 li, +16) = LDS dwords from 592 + 64 wi + 4 li, shifted by 2
-            const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 4 * li;
-            const v4u q = *(const v4u*)(L.B + d0);
-            const uint32_t q4 = L.B[d0 + 4];
-            E[p][0] = __builtin_amdgcn_alignbyte(q.y, q.x, 2);
-            E[p][1] = __builtin_amdgcn_alignbyte(q.z, q.y, 2);
-            E[p][2] = __builtin_amdgcn_alignbyte(q.w, q.z, 2);
-            E[p][3] = __builtin_amdgcn_alignbyte(q4, q.w, 2);
+        const uint32_t wi = WPP * p + g;
+#pragma unroll
+        for (int e = 0; e < 8; e++) E[p][e] = 0;
+        if (WPP * p < nw) {  // (uniform)
+          if (wi < nw) {  // (uniform over the window's 8 lanes)
+            // DD-output bytes [256 wi + 32 li, +32) = LDS dwords from 592 + 64 wi + 8 li, shifted by 2
+            const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 8 * li;
+            const v4u q0 = *(const v4u*)(L.B + d0), q1 = *(const v4u*)(L.B + d0 + 4);
+            const uint32_t q8 = L.B[d0 + 8];
+            const uint32_t Q[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
+#pragma unroll
+            for (int e = 0; e < 8; e++) E[p][e] = __builtin_amdgcn_alignbyte(Q[e + 1], Q[e], 2);
             const uint32_t nb = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
             const uint32_t ne = nb >> 2;
             uint32_t mn32 = SGN ? 0x7fffffffu : 0xffffffffu, mx32 = SGN ? 0x80000000u : 0u;
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-              if (4 * li + e < ne) {
+            for (int e = 0; e < 8; e++) {
+              if (8 * li + e < ne) {
                 const uint32_t v = E[p][e];
                 if (SGN) {
                   mn32 = (int32_t)v < (int32_t)mn32 ? v : mn32;
@@ -340,7 +351,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
                 }
               }
             }
-            row_minmax<SGN>(mn32, mx32);
+            half_minmax<SGN>(mn32, mx32);
             const int64_t mn = ext32<SGN>(mn32), mxv = ext32<SGN>(mx32);
             if (li == 0) {
               // compute_bits_required (bit_width_reduction_filter.cc:406-447)
@@ -423,24 +434,31 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       // ---- compressed windows, in place below the DD output ----
 #pragma unroll
       for (uint32_t p = 0; p < PASSES; p++) {
-        const uint32_t wi = 32 * p + g;
-        if (32 * p < nw && wi < nw) {
+        const uint32_t wi = WPP * p + g;
+        if (WPP * p < nw && wi < nw) {
           const uint32_t off = L.wcs[wi], bits = L.wbits[wi];
           const uint32_t nbw = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
           const uint32_t kind = (bits >= 32 || (nbw & 3) != 0) ? 2u : bits == 8 ? 0u : 1u;
           const uint32_t mnv = (uint32_t)L.wmin[wi];
           const uint32_t a = X0 + off;  // 4-aligned: every earlier window's size is a multiple of 4
-          if (kind == 0) {
-            uint32_t x = 0;
+          uint32_t r[8];
 #pragma unroll
-            for (int e = 0; e < 4; e++) x |= ((E[p][e] - mnv) & 0xffu) << (8 * e);
-            L.B[(a >> 2) + li] = x;
-          } else if (kind == 1) {
-            const uint32_t x0 = ((E[p][0] - mnv) & 0xffffu) | ((E[p][1] - mnv) << 16);
-            const uint32_t x1 = ((E[p][2] - mnv) & 0xffffu) | ((E[p][3] - mnv) << 16);
+          for (int e = 0; e < 8; e++) r[e] = E[p][e] - mnv;
+          if (kind == 0) {
+            uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              x0 |= (r[e] & 0xffu) << (8 * e);
+              x1 |= (r[4 + e] & 0xffu) << (8 * e);
+            }
             *(uint2*)(L.B + (a >> 2) + 2 * li) = make_uint2(x0, x1);
+          } else if (kind == 1) {
+            *(v4u*)(L.B + (a >> 2) + 4 * li) =
+                v4u{(r[0] & 0xffffu) | (r[1] << 16), (r[2] & 0xffffu) | (r[3] << 16), (r[4] & 0xffffu) | (r[5] << 16),
+                    (r[6] & 0xffffu) | (r[7] << 16)};
           } else {
-            *(v4u*)(L.B + (a >> 2) + 4 * li) = v4u{E[p][0], E[p][1], E[p][2], E[p][3]};
+            *(v4u*)(L.B + (a >> 2) + 8 * li) = v4u{E[p][0], E[p][1], E[p][2], E[p][3]};
+            *(v4u*)(L.B + (a >> 2) + 8 * li + 4) = v4u{E[p][4], E[p][5], E[p][6], E[p][7]};
           }
         }
       }
