@@ -18,7 +18,7 @@ for CFG in $CFGS; do
   timeout -k 10 200 python3 -u bench.py --config $CFG --cpu-seconds 5 > $OUT/bench_$CFG.log 2>&1 || { echo "bench $CFG failed"; tail -20 $OUT/bench_$CFG.log; exit 11; }
   tail -1 $OUT/bench_$CFG.log
   for V in ${VARS[$CFG]}; do
-    B="$R/bench.py --config $CFG --variants $V --no-cpu-baseline --no-e2e"
+    B="$R/bench.py --config $CFG --variants $V --no-cpu-baseline --no-e2e --no-others --no-forward"
     timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_${CFG}_$V -o run -- python3 $B --steps 20 --warmup 3 > $OUT/trace_${CFG}_$V.log 2>&1 || { echo "trace $CFG $V failed"; tail -20 $OUT/trace_${CFG}_$V.log; exit 12; }
     for C in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_${CFG}_${V}_$C -o run -- python3 $B --steps 10 --warmup 2 > $OUT/pmc_${CFG}_${V}_$C.log 2>&1 || { echo "pmc $CFG $V $C failed"; tail -20 $OUT/pmc_${CFG}_${V}_$C.log; exit 13; }

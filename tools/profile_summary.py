@@ -99,7 +99,9 @@ def main(out):
                 res[h]["rocprof_roofline_frac"] = round(ach / PEAK, 4)
             if "hbm_bytes_per_launch" in res[h]:
                 res[h]["traffic_over_algorithmic"] = round(res[h]["hbm_bytes_per_launch"] / b_alg, 4)
-        res[f"{cfg}_{line['config']['variant']}"]["bench_line"] = line
+        head = line["config"]["variant"]
+        head = head.split("'")[1] if "'" in head else head  # "min over a,b = 'a'"
+        res[f"{cfg}_{head}"]["bench_line"] = line
     json.dump(res, sys.stdout, indent=1)
     print()
 
