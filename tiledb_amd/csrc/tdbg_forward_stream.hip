@@ -329,9 +329,14 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         if (WPP * p < nw) {  // (uniform)
           if (wi < nw) {  // (uniform over the window's 8 lanes)
             // DD-output bytes [256 wi + 32 li, +32) = LDS dwords from 592 + 64 wi + 8 li, shifted by 2
+            // (windows 2, 3 mod 4 read their second half first: every
+            // ds_read_b128 lane group then covers 64 distinct banks)
             const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 8 * li;
-            const v4u q0 = *(const v4u*)(L.B + d0), q1 = *(const v4u*)(L.B + d0 + 4);
+            const uint32_t hs = 4 * ((wi >> 1) & 1);
+            const v4u qa = *(const v4u*)(L.B + d0 + hs), qb = *(const v4u*)(L.B + d0 + 4 - hs);
             const uint32_t q8 = L.B[d0 + 8];
+            const bool sw = hs != 0;
+            const v4u q0 = sw ? qb : qa, q1 = sw ? qa : qb;
             const uint32_t Q[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
 #pragma unroll
             for (int e = 0; e < 8; e++) E[p][e] = __builtin_amdgcn_alignbyte(Q[e + 1], Q[e], 2);
@@ -466,13 +471,23 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       pc.mark(5);
       if (ok) {
         // ---- store: image bytes [S0, S0 + total) to out, 16-B lane units ----
-        const uint32_t s3 = S0 & 3, sd = S0 >> 2;
+        // (two aligned ds_read_b128 per lane -- lane-consecutive, conflict-free --
+        // shifted by the image's start within its 16-B unit)
+        const uint32_t s16 = S0 & 15, k0 = S0 >> 4, r = s16 & 3, qd = s16 >> 2;
         const uint32_t nu = (total + 15) >> 4;
         for (uint32_t u = T; u < nu; u += NT) {
-          const uint32_t* p = L.B + sd + 4 * u;
-          const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
-          const v4u y{__builtin_amdgcn_alignbyte(d1, d0, s3), __builtin_amdgcn_alignbyte(d2, d1, s3),
-                      __builtin_amdgcn_alignbyte(d3, d2, s3), __builtin_amdgcn_alignbyte(d4, d3, s3)};
+          const v4u A = *(const v4u*)(L.B + 4 * (k0 + u)), Bq = *(const v4u*)(L.B + 4 * (k0 + u + 1));
+          const uint32_t W8[8] = {A.x, A.y, A.z, A.w, Bq.x, Bq.y, Bq.z, Bq.w};
+          v4u y;
+          switch (qd) {  // (uniform)
+#define TDBG_SH(q)                                                                                   \
+  case q:                                                                                            \
+    y = v4u{__builtin_amdgcn_alignbyte(W8[q + 1], W8[q], r), __builtin_amdgcn_alignbyte(W8[q + 2], W8[q + 1], r), \
+            __builtin_amdgcn_alignbyte(W8[q + 3], W8[q + 2], r), __builtin_amdgcn_alignbyte(W8[q + 4], W8[q + 3], r)}; \
+    break;
+            TDBG_SH(0) TDBG_SH(1) TDBG_SH(2) default: TDBG_SH(3)
+#undef TDBG_SH
+          }
           if (16 * u + 16 <= total) {
             __builtin_nontemporal_store(y, (g_u4*)(out + 16 * u));
           } else {
