@@ -193,7 +193,8 @@ __device__ __forceinline__ void dd_codes(const uint32_t (&G)[20], uint32_t p, ui
   for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
   // M_j = p ? H[(j+1)^1] : H[j^1] as a bit select (v_bfi_b32): a plain
   // ternary lets the optimizer turn the pair into an indexed scratch load
-  const uint32_t pm = 0u - p;
+  uint32_t pm = 0u - p;
+  asm volatile("" : "+v"(pm));  // (opaque: the select stays one v_bfi_b32, not a cndmask + and_or)
   uint32_t M[17];
 #pragma unroll
   for (int j = 0; j < 17; j++) M[j] = (pm & H[(j + 1) ^ 1]) | (~pm & H[j ^ 1]);
