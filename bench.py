@@ -3,17 +3,18 @@
 
 Workload (BASELINE.json configs[4]): dense int32 tiles of
 64 KiB (one chunk each), pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)],
-12,500 tiles per GPU (C5's 100k tiles over 8 GPUs; weak scaling).  The other
-configs run with --config c1|c2|c2i|c3a|c3b|c4 (one JSON line each).  A step
-is one unfilter pass (one tdbg_unfilter_tiles_async launch) over the rank's
-12,500 resident tiles, packed back to back in HBM at arbitrary byte offsets
+the config's 100,000 tiles sharded over the N GPUs (strong scaling: at N = 1
+all 100,000 are resident on the one GPU, at N = 8 each GPU holds 12,500).
+The other configs run with --config c1|c2|c2i|c3a|c3b|c4 (one JSON line each).
+A step is one unfilter pass (one tdbg_unfilter_tiles_async launch) over the
+rank's resident tiles, packed back to back in HBM at arbitrary byte offsets
 (as FilteredData hands them over, filtered_data.h:100-101).
 
-The headline `value` is the "active" data variant, the one where all three
-stages do work (DoubleDelta bit-packed, BWR windows 8-bit, byteshuffle);
-"rand" (DD and BWR raw: two stages are views) and "ramp" (DD raw) are
-reported beside it, with the minimum over the three.  Every timed launch's
-statuses and every output tile are checked after the timed region.
+Three data variants: "rand" (DD and BWR raw: two stages are views) and
+"ramp" (DD raw) are SURVEY's; "active" makes all three stages work
+(DoubleDelta bit-packed, BWR windows 8-bit, byteshuffle).  `value` is the
+minimum over the three.  Every timed launch's statuses and every output tile
+are checked after the timed region.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N   (one rank per GPU)
@@ -50,9 +51,11 @@ CONFIGS = {
     "c4": dict(tiles_per_gpu=12500, variants="offsets", dtype="uint64",
                workload="C4: var-length offsets uint64, [POSITIVE_DELTA(1024), BIT_WIDTH_REDUCTION(256)], "
                         "50k tiles / 4 GPUs"),
-    "c5": dict(tiles_per_gpu=12500, variants="active,rand,ramp", dtype="int32",
+    # the metric's config: 100,000 tiles in all, sharded over the N GPUs
+    # (strong scaling; at N = 1 the whole config is resident on the one GPU)
+    "c5": dict(tiles_per_gpu=12500, total_tiles=100000, variants="active,rand,ramp", dtype="int32",
                workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
-                        "64 KiB tiles (1 chunk), device-resident, 100k tiles / 8 GPUs"),
+                        "64 KiB tiles (1 chunk), device-resident, 100k tiles sharded over the GPUs"),
     "c5big": dict(tiles_per_gpu=200, variants="active", dtype="int32",
                   workload="C5 pipeline, 4 MiB tiles (64 chunks of 64 KiB), 200 tiles per GPU: "
                            "chunk-parallel launch (device chunk directory)"),
@@ -220,6 +223,13 @@ def max_over_ranks(dist, x: float, device: str) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(dist, x: float, device: str) -> float:
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -296,20 +306,24 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
             verify(batch, vals, idx)
         unf = float(sum(vals[i].nbytes for i in idx))
         b_alg = float(sizes.sum()) + unf
-        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf,
+        unf_job = sum_over_ranks(dist, unf, DIST_DEV) if dist is not None else unf
+        res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf, unf_job=unf_job,
                         out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback, streamed=streamed,
                         packed=packed, offs=offs, sizes=sizes, steps=steps, ntiles=ntiles)
         if forward and vi == 0 and not ablation and cfgname != "fscale":  # (lossy: values differ)
             res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, steps, warmup, dist)
         if e2e_leg:
-            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs, sizes, int(vals[0].nbytes), args, dist, world)
+            ne = min(ntiles, args.e2e_tiles) if args.e2e_tiles else ntiles
+            res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs[:ne], sizes[:ne], int(vals[0].nbytes), args, dist,
+                                  world)
         del batch
         torch.cuda.empty_cache()
     return dp, res
 
 
 def gibps(r, world):
-    return r["unf"] * world / (r["elapsed"] / r["steps"]) / 2**30
+    # unfiltered bytes of the whole job (every rank's shard) / max-over-ranks time
+    return r.get("unf_job", r["unf"] * world) / (r["elapsed"] / r["steps"]) / 2**30
 
 
 def frac(r):
@@ -389,7 +403,7 @@ def headline_line(args, W, variants, res, world):
         "warmup": args.warmup,
         "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if "total_tiles" in cfg and not args.tiles_per_gpu else "weak",
         "vs_baseline": None,
         "dtype": cfg["dtype"],
         "data": f"synthetic {args.config.upper()} tiles, variants {','.join(variants)} ({args.unique} unique each, "
@@ -456,7 +470,7 @@ def main():
     ap.add_argument("--config", default="c5", choices=sorted(CONFIGS),
                     help="BASELINE config (default C5, the metric's 3-stage pipeline)")
     ap.add_argument("--tiles-per-gpu", type=int, default=0,
-                    help="default: the config's per-GPU tile count (C5: 100k / 8)")
+                    help="default: the config's per-GPU tile count (C5: its 100,000 tiles / N)")
     ap.add_argument("--unique", type=int, default=128)
     ap.add_argument("--variants", default="")
     ap.add_argument("--align", type=int, default=1,
@@ -473,13 +487,16 @@ def main():
     ap.add_argument("--forward", action="store_true", default=True,
                     help="also time the forward (filter) direction on the first variant (default on)")
     ap.add_argument("--no-forward", dest="forward", action="store_false")
+    ap.add_argument("--e2e-tiles", type=int, default=25000,
+                    help="host E2E leg on the first N tiles of the rank's shard (0 = all; PCIe-bound)")
     ap.add_argument("--e2e-batch-mb", type=int, default=64,
                     help="host E2E staging batch (MiB per side; 2 batches in flight)")
     ap.add_argument("--others", action="store_true", default=True,
                     help="N = 1 default C5 run: also time every other BASELINE config (config.other_configs) "
                          "and C5 at 100k tiles on the one GPU")
     ap.add_argument("--no-others", dest="others", action="store_false")
-    ap.add_argument("--big-tiles", type=int, default=100000, help="tiles of the single-GPU C5 leg")
+    ap.add_argument("--shard-tiles", type=int, default=12500,
+                    help="N = 1 run: also time C5 on one GPU's shard of an 8-GPU node (100k / 8)")
     args = ap.parse_args()
 
     import torch
@@ -498,7 +515,15 @@ def main():
     import workloads as W
 
     cfg = CONFIGS[args.config]
-    ntiles = args.tiles_per_gpu or cfg["tiles_per_gpu"]
+    if args.tiles_per_gpu:
+        ntiles = args.tiles_per_gpu
+    elif "total_tiles" in cfg:
+        # strong scaling: the config's tiles, sharded over the ranks (rank r
+        # takes tiles [r * n, (r + 1) * n) of the job; the last may be short)
+        per = -(-cfg["total_tiles"] // world)
+        ntiles = max(1, min(per, cfg["total_tiles"] - rank * per))
+    else:
+        ntiles = cfg["tiles_per_gpu"]
     ctx = engine.Context(torch.cuda.current_device())  # this rank's GPU (set above)
     variants = [v for v in (args.variants or cfg["variants"]).split(",") if v]
     dp, res = run_config(engine, ctx, W, args, args.config, variants, ntiles, args.steps, args.warmup, dist,
@@ -530,19 +555,19 @@ def main():
             for v in cres:  # free the host copies
                 cres[v].pop("packed", None)
         line["config"]["other_configs"] = others
-        # C5 at its full BASELINE size (100k tiles) on this one GPU
-        big = {}
-        _, bres = run_config(engine, ctx, W, args, "c5", variants, args.big_tiles, max(3, args.steps // 4),
-                             2, dist, world, rank)
-        for v in variants:
-            # (no PMC pass of this 100k-tile workload is committed: traffic null,
-            # not the 12,500-tile or 4 MiB-tile figure)
-            big[v] = variant_line("c5_100k", v, bres[v], world)
-            bres[v].pop("packed", None)
-        line["config"]["c5_100k_single_gpu"] = {
-            "tiles": args.big_tiles, "steps": max(3, args.steps // 4), "variants": big,
-            "min_over_variants_GiBps": round(min(x["GiBps"] for x in big.values()), 2),
-            "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in big.values()), 4)}
+        # C5 on one GPU's shard of the 8-GPU config (12,500 tiles): the
+        # per-GPU work of the N = 8 line
+        if args.shard_tiles and args.shard_tiles != ntiles:
+            sh = {}
+            _, sres = run_config(engine, ctx, W, args, "c5", variants, args.shard_tiles, args.steps,
+                                 args.warmup, dist, world, rank)
+            for v in variants:
+                sh[v] = variant_line("c5shard", v, sres[v], world)
+                sres[v].pop("packed", None)
+            line["config"]["c5_shard_12500"] = {
+                "tiles": args.shard_tiles, "steps": args.steps, "variants": sh,
+                "min_over_variants_GiBps": round(min(x["GiBps"] for x in sh.values()), 2),
+                "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sh.values()), 4)}
     if rank == 0 and not args.no_cpu_baseline:
         # after every timed region, at any N (rank 0 only)
         line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds)
@@ -569,7 +594,7 @@ def e2e(engine, ctx, dp, packed, offs, sizes, out_bytes, args, dist=None, world=
     batch) and the results in one pinned result buffer."""
     import torch
     n = offs.size
-    hin = torch.from_numpy(packed).pin_memory()
+    hin = torch.from_numpy(packed[: int(offs[-1] + sizes[-1])]).pin_memory()
     hout = torch.empty(n * out_bytes, dtype=torch.uint8).pin_memory()
     in_ptrs = offs + np.uint64(hin.data_ptr())
     out_ptrs = np.arange(n, dtype=np.uint64) * np.uint64(out_bytes) + np.uint64(hout.data_ptr())

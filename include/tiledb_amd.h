@@ -113,8 +113,10 @@ enum tdbg_status {
                                float datatypes." delta_compressor.cc:210-213   */
   TDBG_E_INTERNAL = 17,     /* internal engine error (a device work queue overflowed):
                                the tile was not unfiltered; never expected   */
-  TDBG_E_IO = 18            /* tdbg_read_unfilter_tiles: a block read failed
+  TDBG_E_IO = 18,           /* tdbg_read_unfilter_tiles: a block read failed
                                (VFS::read_exactly: short read or I/O error)  */
+  TDBG_E_NOT_RUN = 19       /* the call stopped (a device or argument error)
+                               before this tile was read or unfiltered       */
 };
 
 /* unfilter flags */
@@ -377,7 +379,7 @@ int tdbg_context_device(const tdbg_context* ctx);
 int tdbg_host_alloc_local(int device, uint64_t bytes, void** out);
 int tdbg_host_free(void* p);
 
-/* FilteredData block rule (filtered_data.h:503-540): tiles in result-tile
+/* FilteredData block rule (filtered_data.h:531-575): tiles in result-tile
  * order, tile i at file_offset[i] (size[i]) of file file_idx[i]; a tile
  * extends the current block when it is in the same file, the block stays <=
  * max_batch_size, and the block is <= min_batch_size or the gap to the tile

@@ -212,7 +212,7 @@ def compute_chunk_size(tile_size: int, cell_size: int, max_chunk: int = 0) -> in
 # ---------------------------------------------------------------------------
 def filtered_data_blocks(file_idx, file_offset, size, min_batch_size: int = 20971520,
                          max_batch_size: int = 104857600, min_batch_gap: int = 512000):
-    """FilteredData::make_new_block_if_required (filtered_data.h:503-540),
+    """FilteredData::make_new_block_if_required (filtered_data.h:531-575),
     one TileType: tiles in result-tile order; a tile extends the current block
     iff same fragment, new_size <= max_batch_size and (new_size <=
     min_batch_size or gap <= min_batch_gap), with the reference's unsigned

@@ -2,7 +2,7 @@
 
 * FilteredData-style reads (tdbg_filtered_data_blocks / tdbg_read_unfilter_tiles):
   the block rule against the oracle's restatement of
-  FilteredData::make_new_block_if_required (filtered_data.h:503-540) on the CPU,
+  FilteredData::make_new_block_if_required (filtered_data.h:531-575) on the CPU,
   and on the GPU tiles read from fragment files by IO threads into
   NUMA-local pinned blocks, unfiltered, bit-exact against the oracle.
 * Dense cell-slab copy fused with the D2H (tdbg_dense_read_host /
@@ -131,6 +131,60 @@ def test_read_unfilter_tiles_from_files(oracle_mod, cfg_kind):
         finally:
             for fd in fds:
                 os.close(fd)
+
+
+@pytest.mark.gpu
+def test_read_unfilter_statuses_after_device_failure(oracle_mod, monkeypatch):
+    """A device error in block 1 (injected: TDBG_DEBUG_IO_FAIL_BLOCK) after a
+    block holding a corrupt tile: block 0 keeps its real statuses (the corrupt
+    tile's error, OK for the rest), every tile of block 1 and after says
+    TDBG_E_NOT_RUN -- never OK for output that was not written -- and the call
+    raises the device error although some tiles carry statuses."""
+    import torch
+    assert torch.cuda.is_available()
+    from tiledb_amd import _native, engine
+    tiles, vals = W.c5_pool("active", 8, seed=7)
+    tiles = [bytearray(t) for t in tiles]
+    tiles[1][8:12] = (70000).to_bytes(4, "little")  # chunk orig size != tile size
+    with tempfile.TemporaryDirectory() as tmp:
+        pth = os.path.join(tmp, "frag.tdb")
+        blob, foff = bytearray(), []
+        for t in tiles:
+            foff.append(len(blob))
+            blob += t
+        with open(pth, "wb") as fh:
+            fh.write(bytes(blob))
+        fd = os.open(pth, os.O_RDONLY)
+        try:
+            ctx = engine.Context(0)
+            dp = engine.DevicePipeline(_c5_pipe(), 23, int(Datatype.INT32), 4)
+            n = len(tiles)
+            res = engine.HostBuffer(0, n * W.TILE_BYTES)
+            out_ptrs = res.ptr + np.arange(n, dtype=np.uint64) * np.uint64(W.TILE_BYTES)
+            cfg = _native.ReadConfig()
+            # blocks of 2 tiles: [0, 1], [2, 3], ...
+            cfg.min_batch_size, cfg.max_batch_size, cfg.min_batch_gap = 1, 2 * max(len(t) for t in tiles), 0
+            cfg.flags = 0x1  # TDBG_READ_ZERO_GAP
+            size = np.array([len(t) for t in tiles], dtype=np.uint64)
+            fidx = np.zeros(n, dtype=np.uint32)
+            nb = oracle_mod.filtered_data_blocks(fidx, np.array(foff, dtype=np.uint64), size,
+                                                                  cfg.min_batch_size, cfg.max_batch_size, 0)
+            assert list(nb[:3]) == [0, 2, 4], nb
+            monkeypatch.setenv("TDBG_DEBUG_IO_FAIL_BLOCK", "1")
+            st = np.full(n, -1, dtype=np.int32)
+            with pytest.raises(engine.EngineError) as ei:
+                ctx.read_unfilter(dp, [fd], fidx, np.array(foff, dtype=np.uint64), size, out_ptrs,
+                                  np.full(n, W.TILE_BYTES, dtype=np.uint64), cfg=cfg, status_out=st)
+            assert ei.value.code == 14  # TDBG_E_DEVICE
+            assert st[0] == 0 and st[1] == 3  # TDBG_E_TILE_SIZE (tile.cc:308)
+            assert (st[2:] == engine.E_NOT_RUN).all(), st
+            assert np.array_equal(res.array[:W.TILE_BYTES], vals[0].view(np.uint8))
+            monkeypatch.delenv("TDBG_DEBUG_IO_FAIL_BLOCK")
+            st = ctx.read_unfilter(dp, [fd], fidx, np.array(foff, dtype=np.uint64), size, out_ptrs,
+                                   np.full(n, W.TILE_BYTES, dtype=np.uint64), cfg=cfg)
+            assert st[1] == 3 and (np.delete(st, 1) == 0).all(), st
+        finally:
+            os.close(fd)
 
 
 # ---------------------------------------------------------------------------

@@ -76,9 +76,11 @@ def _worker(rank: int, world: int, port: int, q):
         offs = np.concatenate([[0], np.cumsum(isz[lo:hi])[:-1]]).astype(np.uint64)
         elapsed = bench.max_over_ranks(dist, el, "cpu")
         r = dict(elapsed=elapsed, kern_ms=el * 1e3, launch_ms=el * 1e3, b_alg=float(isz[lo:hi].sum() + osz[lo:hi].sum()),
-                 unf=float(osz[lo:hi].sum()), out_bytes=W.TILE_BYTES, fused=hi - lo, fallback=0, streamed=hi - lo,
+                 unf=float(osz[lo:hi].sum()), unf_job=bench.sum_over_ranks(dist, float(osz[lo:hi].sum()), "cpu"),
+                 out_bytes=W.TILE_BYTES, fused=hi - lo, fallback=0, streamed=hi - lo,
                  packed=packed, offs=offs, sizes=isz[lo:hi], steps=1, ntiles=hi - lo)
-        args = argparse.Namespace(config="c5", warmup=0, unique=len(tiles), align=1, e2e_batch_mb=64)
+        args = argparse.Namespace(config="c5", warmup=0, unique=len(tiles), align=1, e2e_batch_mb=64,
+                                  tiles_per_gpu=0)
         line = bench.headline_line(args, W, ["rand"], {"rand": r}, world)
         if rank == 0:
             line["cpu_baseline"] = bench.cpu_line(engine, dp, r, "c5", "rand", 2, 0.2)
@@ -110,7 +112,10 @@ def test_two_rank_shards_cover_every_tile_once():
         assert digests[i] == int(vals[i].view(np.uint32).astype(np.uint64).sum()) + 1
     assert slow == 2.0
     # the N = 2 line: whole-job value over both ranks, roofline, CPU baseline
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
+    # C5's 100k tiles sharded over the ranks: strong scaling, the whole job's bytes
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    job = sum(len(v) * 4 for v in vals)
+    assert abs(line["value"] - job / (line["ms_per_step"] * 1e-3) / 2**30) < 1e-3 * line["value"] + 0.01
     assert line["roofline"]["bound"] == "hbm" and 0 < line["roofline"]["frac"]
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0 and cb["unit"] == "GiB/s"

@@ -316,8 +316,9 @@ def test_small_wrong_sizes_and_offsets(eng, ctx, oracle_mod, cfg):
 @pytest.mark.parametrize("align", [1, 16])
 @pytest.mark.parametrize("ntiles", [7, 256, 700])
 def test_shuffle4_config_tiles(eng, ctx, oracle_mod, ntiles, align):
-    """SURVEY's C1 tiles (ramp and rand), back to back or 16-B aligned, also
-    fewer tiles than CUs: every one taken by the unit-parallel kernel."""
+    """SURVEY's C1 tiles (ramp and rand), back to back or 16-B aligned: every
+    one taken by the unit-parallel kernel; a batch of fewer tiles than CUs runs
+    chunk-parallel (the device chunk directory), as any pipeline's does."""
     from tests.test_gpu_parity import check_parity, encode
     from tests.cases import c1_tiles
     from tiledb_amd.filter_pipeline import ByteshuffleFilter
@@ -331,7 +332,29 @@ def test_shuffle4_config_tiles(eng, ctx, oracle_mod, ntiles, align):
                  align=align)
     f1, b1, _ = ctx.path_stats()
     assert b1 - b0 == 0 and f1 - f0 == ntiles
-    assert ctx.stream_tiles() - s0 == ntiles
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert ctx.stream_tiles() - s0 == (ntiles if ntiles >= cus else 0)
+
+
+def test_shuffle4_few_multichunk_tiles_chunk_parallel(eng, ctx, oracle_mod):
+    """A few multi-chunk [BYTESHUFFLE] int32 tiles (1 MiB = 16 chunks each,
+    fewer tiles than CUs): the launch runs chunk-parallel, not on the
+    unit-parallel kernel (which takes only one-chunk tiles), so every chunk is
+    its own work item; bit-exact vs the oracle."""
+    from tests.test_gpu_parity import check_parity, encode
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter
+    rng = np.random.default_rng(64)
+    tiles = [as_u8(rng.integers(-2**31, 2**31, 262144 - 7 * k, dtype=np.int64).astype(np.int32)) for k in range(4)]
+    case = Case("c1_multichunk", P(ByteshuffleFilter()), Datatype.INT32, 4, tiles)
+    _, enc = encode(oracle_mod, case)
+    assert all(int(np.frombuffer(e[0][:8].tobytes(), dtype=np.uint64)[0]) == 16 for e in enc)
+    f0, b0, _ = ctx.path_stats()
+    s0 = ctx.stream_tiles()
+    check_parity(eng, ctx, oracle_mod, case, [e[0] for e in enc], [e[2] for e in enc], [e[1] for e in enc])
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0 and f1 - f0 == len(tiles)
+    assert ctx.stream_tiles() == s0
 
 
 def test_shuffle4_declined_tiles(eng, ctx, oracle_mod):

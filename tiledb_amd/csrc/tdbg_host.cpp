@@ -410,6 +410,7 @@ const char* tdbg_status_str(int s) {
     case TDBG_E_DELTA_TYPE: return "Decompression is not yet supported for float datatypes.";
     case TDBG_E_INTERNAL: return "internal: device work queue overflow";
     case TDBG_E_IO: return "tile read failed (short read or I/O error)";
+    case TDBG_E_NOT_RUN: return "tile not processed: the call stopped on an earlier error";
     default: return "unknown";
   }
 }
@@ -642,11 +643,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
   static const bool tile_mode = getenv("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
-  // [BYTESHUFFLE] on 4-byte values (C1): the unit-parallel streaming kernel
-  // (tdbg_stream_shuffle.hip) splits every tile over 16 workgroups itself
-  const bool shuffle4 = p->plan.fast == 1 && p->plan.nstages == 1 && p->plan.s[0].w == 4;
   const bool chunked = queued && !d_list &&
-                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && !shuffle4 && ntiles < (uint64_t)c->cus));
+                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
+  // [BYTESHUFFLE] on 4-byte values (C1): the unit-parallel streaming kernel
+  // (tdbg_stream_shuffle.hip) splits every one-chunk 64 KiB tile over 16
+  // workgroups itself; batches of fewer tiles than CUs (e.g. a few
+  // multi-chunk tiles, which that kernel declines) stay chunk-parallel
+  const bool shuffle4 = !chunked && p->plan.fast == 1 && p->plan.nstages == 1 && p->plan.s[0].w == 4;
   // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.

@@ -7,7 +7,7 @@
 // and a tile extends the current block when it is in the same file, the
 // block stays <= max_batch_size, and either the block is still <=
 // min_batch_size or the gap to the tile is <= min_batch_gap
-// (make_new_block_if_required, filtered_data.h:503-540; defaults
+// (make_new_block_if_required, filtered_data.h:531-575; defaults
 // vfs.min_batch_size 20 MiB, vfs.max_batch_size 100 MiB, vfs.min_batch_gap
 // 500 KB, config.cc:163-165).  Every block is read with VFS::read_exactly on
 // the IO thread pool (filtered_data.h:397-398) and tiles point into it
@@ -27,6 +27,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -172,7 +173,8 @@ int tdbg_read_unfilter_tiles(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     bsz[b] = hi - lo;
     maxb = std::max(maxb, bsz[b]);
   }
-  // pinned slots on the GPU's NUMA node, kept for later calls
+  // pinned slots on the GPU's NUMA node (allocated per call: nslots x the
+  // largest block, first-touched on the device's node)
   std::vector<void*> slot(nslots, nullptr);
   for (uint32_t k = 0; k < nslots; k++) {
     r = tdbg_host_alloc_local(tdbg_context_device(c), maxb, &slot[k]);
@@ -221,7 +223,13 @@ int tdbg_read_unfilter_tiles(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   }
   int result = TDBG_OK;
   std::string err;
-  std::vector<int32_t> st(ntiles, 0);
+  // test hook: block k's unfilter "fails" with a device error before any of
+  // its statuses exist (the failure class of a HIP error in the host path)
+  const long fail_block = getenv("TDBG_DEBUG_IO_FAIL_BLOCK") ? atol(getenv("TDBG_DEBUG_IO_FAIL_BLOCK")) : -1;
+  // every tile is "not processed" until its block's unfilter reports it: a
+  // block whose unfilter stops early (a device error before its statuses
+  // are copied back), and every block after a device error, keep that
+  std::vector<int32_t> st(ntiles, TDBG_E_NOT_RUN);
   std::vector<const uint8_t*> in(ntiles);
   for (uint64_t b = 0; b < nb; b++) {
     {
@@ -238,9 +246,11 @@ int tdbg_read_unfilter_tiles(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
     } else {
       const uint8_t* base = (const uint8_t*)slot[b % nslots];
       for (uint64_t i = lo; i < hi; i++) in[i] = base + (file_offset[i] - boff[b]);
-      const int rr = tdbg_unfilter_tiles_host(c, p, hi - lo, in.data() + lo, persisted_size + lo, out + lo,
-                                              out_size + lo, flags | TDBG_HOST_CONTIGUOUS_INPUT, st.data() + lo,
-                                              0);
+      const int rr =
+          (long)b == fail_block
+              ? (tdbg_internal_set_error("injected device failure (TDBG_DEBUG_IO_FAIL_BLOCK)"), TDBG_E_DEVICE)
+              : tdbg_unfilter_tiles_host(c, p, hi - lo, in.data() + lo, persisted_size + lo, out + lo, out_size + lo,
+                                         flags | TDBG_HOST_CONTIGUOUS_INPUT, st.data() + lo, 0);
       if (rr && result == TDBG_OK) {
         result = rr;
         char buf[512];

@@ -24,6 +24,9 @@ TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
 HOST_CONTIGUOUS_INPUT = 0x2   # TDBG_HOST_CONTIGUOUS_INPUT
 HOST_CONTIGUOUS_OUTPUT = 0x4  # TDBG_HOST_CONTIGUOUS_OUTPUT
 CHUNK_PARALLEL = 0x8  # TDBG_CHUNK_PARALLEL
+E_NOT_RUN = 19  # TDBG_E_NOT_RUN
+# call-level failures (not a tile's status): raised even when tiles carry statuses
+CALL_ERRORS = (1, 10, 14, 15, 17)  # TDBG_E_ARG, _UNSUPPORTED, _DEVICE, _DESCRIPTOR, _INTERNAL
 
 
 class EngineError(RuntimeError):
@@ -375,9 +378,10 @@ class Context:
         torch.cuda.synchronize(batch.d_out.device)
 
     def read_unfilter(self, dp: DevicePipeline, fds, file_idx, file_offset, size, out_ptrs, out_sizes,
-                       flags: int = 0, cfg=None) -> np.ndarray:
+                       flags: int = 0, cfg=None, status_out: Optional[np.ndarray] = None) -> np.ndarray:
         """tdbg_read_unfilter_tiles: FilteredData-style block reads from the open
-        files `fds` -> H2D -> unfilter -> D2H into out_ptrs; per-tile statuses."""
+        files `fds` -> H2D -> unfilter -> D2H into out_ptrs; per-tile statuses
+        (also copied into status_out, if given, before a call-level error raises)."""
         n = int(np.asarray(size).size)
         st = np.zeros(max(n, 1), dtype=np.int32)
         fd = np.ascontiguousarray(fds, dtype=np.int32)
@@ -390,7 +394,11 @@ class Context:
                                           sz.ctypes.data, op.ctypes.data, osz.ctypes.data, flags,
                                           ctypes.byref(cfg) if cfg is not None else None,
                                           st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
-        if rc and not st[:n].any():
+        if status_out is not None:
+            status_out[:n] = st[:n]
+        # call-level failures raise even when some tiles carry statuses (those
+        # after the failure say TDBG_E_NOT_RUN); tile-level ones are in st
+        if rc and (rc in CALL_ERRORS or not st[:n].any()):
             _check(rc, "tdbg_read_unfilter_tiles")
         return st[:n]
 
@@ -409,7 +417,7 @@ class Context:
         rc = lib.tdbg_dense_read_host(self.h, dp.h, n, ip.ctypes.data, isz.ctypes.data, ts.ctypes.data,
                                       ctypes.byref(cfg), result.ctypes.data, result.size, flags,
                                       st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), batch_bytes)
-        if rc and not st[:n].any():
+        if rc and (rc in CALL_ERRORS or not st[:n].any()):
             _check(rc, "tdbg_dense_read_host")
         return st[:n]
 
@@ -489,7 +497,7 @@ def device_count() -> int:
 # ---------------------------------------------------------------------------
 def filtered_data_blocks(file_idx, file_offset, size, min_batch_size: int = 20971520,
                          max_batch_size: int = 104857600, min_batch_gap: int = 512000) -> np.ndarray:
-    """FilteredData blocks (filtered_data.h:503-540) of tiles in result-tile
+    """FilteredData blocks (filtered_data.h:531-575) of tiles in result-tile
     order: the first tile of every block, then ntiles."""
     fi = np.ascontiguousarray(file_idx, dtype=np.uint32)
     fo = np.ascontiguousarray(file_offset, dtype=np.uint64)
