@@ -107,6 +107,50 @@ def test_fused_spec_no_fallback(eng, ctx, oracle_mod, case, align):
     del dp
 
 
+def check_parity_replicated(eng, ctx, O, case, enc, n, align=1):
+    """n tiles cycling over the unique encoded tiles `enc` (the oracle runs
+    once per unique tile): a launch of more tiles than the GPU has CUs, so it
+    takes the tile-serial path (fused kernel: cross-tile prefetch and the
+    load hook; or the streaming kernels), not the chunk-parallel one."""
+    op = O.OraclePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
+    refs = [op.unfilter_tile(e[0], e[2], case.offsets_tile) for e in enc]
+    idx = np.arange(n) % len(enc)
+    batch = eng.TileBatch.from_host([enc[i][0] for i in idx], [enc[i][2] for i in idx], align=align)
+    st = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile)
+    out = batch.outputs_host()
+    for k, i in enumerate(idx):
+        rc, ref = refs[i]
+        assert int(st[k]) == rc, f"{case.name} tile {k}: gpu status {st[k]} oracle {rc}"
+        if rc == 0:
+            o = int(batch.out_off[k])
+            assert np.array_equal(out[o:o + enc[i][2]], ref), f"{case.name} tile {k} differs from the oracle"
+    return st
+
+
+# the tile-serial launch of the fused kernel (tdbg_fast.hip: one tile per
+# workgroup iteration, next tile prefetched, stage hooks) and the streaming
+# kernels run only when a launch has at least one tile per CU
+_SERIAL_N = 320
+
+
+@pytest.mark.parametrize("case", _CONFIG + _SPECS, ids=[c.name for c in _CONFIG + _SPECS])
+def test_tile_serial_launch_parity(eng, ctx, oracle_mod, case):
+    """Every BASELINE config and one case per fused spec at 320 tiles:
+    bit-exact vs the oracle, every tile taken by the fused/streaming kernels
+    (fallback == 0, fused == 320)."""
+    import torch
+    assert _SERIAL_N >= torch.cuda.get_device_properties(0).multi_processor_count
+    _, enc = encode(oracle_mod, case)
+    assert enc
+    f0, b0, _ = ctx.path_stats()
+    st = check_parity_replicated(eng, ctx, oracle_mod, case, enc, _SERIAL_N)
+    assert not st.any()
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0, f"{case.name}: {b1 - b0} tiles fell back to the general path"
+    assert f1 - f0 == _SERIAL_N
+
+
 @pytest.mark.parametrize("case", _EDGE, ids=[c.name for c in _EDGE])
 def test_edge_parity(eng, ctx, oracle_mod, case):
     _, enc = encode(oracle_mod, case)

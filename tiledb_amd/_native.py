@@ -15,6 +15,10 @@ except Exception:  # pragma: no cover - torch is optional for pure C-ABI use
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtiledb_amd.so")
+# experiments only: TDBG_LIB names another in-tree build of the same C-ABI
+# (e.g. the previous commit's kernels, for same-box A/B timing)
+if os.environ.get("TDBG_LIB"):
+    LIB_PATH = os.path.join(_HERE, os.environ["TDBG_LIB"])
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

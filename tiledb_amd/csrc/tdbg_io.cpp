@@ -251,7 +251,11 @@ int tdbg_read_unfilter_tiles(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
               ? (tdbg_internal_set_error("injected device failure (TDBG_DEBUG_IO_FAIL_BLOCK)"), TDBG_E_DEVICE)
               : tdbg_unfilter_tiles_host(c, p, hi - lo, in.data() + lo, persisted_size + lo, out + lo, out_size + lo,
                                          flags | TDBG_HOST_CONTIGUOUS_INPUT, st.data() + lo, 0);
-      if (rr && result == TDBG_OK) {
+      // the first failure wins, except that a call-level failure (device,
+      // argument, internal) replaces a tile's: the statuses then do not
+      // account for every tile (those not run say TDBG_E_NOT_RUN)
+      const auto call_level = [](int s) { return s == TDBG_E_DEVICE || s == TDBG_E_ARG || s == TDBG_E_INTERNAL; };
+      if (rr && (result == TDBG_OK || (call_level(rr) && !call_level(result)))) {
         result = rr;
         char buf[512];
         tdbg_last_error(buf, sizeof(buf));

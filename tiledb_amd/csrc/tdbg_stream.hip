@@ -70,8 +70,9 @@ struct Lds {
   uint2 TAB[TABN];                   // {LDS byte address | kind << 16, window minimum}
   uint32_t WS[NWV][WSD];
   uint32_t red[4][NWV][2];           // per plane and wave: DD aggregate (A, B)
+  uint32_t wt[NWV];                  // compressed bytes of each wave's 64 windows
   uint32_t vd[NWV];                  // each wave's header verdict (ANDed after B2)
-  uint32_t vok[NWV];                 // each wave's DD-header verdict (ANDed after B3)
+  uint32_t vok[NWV];                 // each wave's DD-header verdict (ANDed after P0)
   uint64_t clk[8];                   // diagnostics: phase clocks (TDBG_PROF)
 };
 
@@ -287,91 +288,139 @@ struct Clock {
   }
 };
 
-// The four planes of one tile for one wave (code width CB): BWR⁻¹ of the
-// wave's range into its scratch, the lane's 16 codes straight into xl[k],
-// the local affine scan and the DPP wave scan; the wave totals go to red.
-template <int CB, bool SGN>
-__device__ __forceinline__ void planes(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
-                                       uint32_t (&xl)[4][16], Clock& pc) {
+// Plane K of one tile for one wave (code width CB): BWR⁻¹ of the wave's
+// range into its scratch, the lane's 16 codes straight into xk (local
+// running values), the local affine scan and the DPP wave scan.  Returns the
+// lane's exclusive wave prefix (ae, be); lane 63 puts the wave total in red.
+// The caller folds prefix and block start into xk after the plane's barrier.
+template <int CB, int K, bool SGN>
+__device__ __forceinline__ void plane(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
+                                      uint32_t (&xk)[16], uint32_t& ae, uint32_t& be, Clock& pc) {
   uint32_t* wsp = L.WS[w];
   constexpr int32_t cb = CB;
+  const int32_t c0w = 4096 * K + 1024 * (int32_t)w - 2;
+  const int32_t P0 = (c0w + 16 * (int32_t)l) * cb;
+  const int32_t b0 = (P0 + 31) >> 5;
+  const uint32_t n = (uint32_t)(32 * b0 - P0);
+  const int32_t Ms = b0 - 1;
+  const uint32_t p = (uint32_t)Ms & 1u;
+  const int32_t es = 8 + 2 * (Ms >> 1);
+  // the wave's range starts at lane 0's first dword
+  const int32_t P00 = c0w * cb;
+  const int32_t es0 = 8 + 2 * ((((P00 + 31) >> 5) - 1) >> 1);
+  const uint32_t ulo = (uint32_t)es0 >> 2;
+  __builtin_amdgcn_wave_barrier();
+  // four rounds of 64 units (the wave needs <= 252 for cb <= 31), batched:
+  // every table entry first, one uniform choice of the unit decoder, then
+  // the reads
+  uint32_t uu[4], wc[4];
+  uint2 te[4];
+  bool gen = false;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int32_t c0w = 4096 * k + 1024 * (int32_t)w - 2;
-    const int32_t P0 = (c0w + 16 * (int32_t)l) * cb;
-    const int32_t b0 = (P0 + 31) >> 5;
-    const uint32_t n = (uint32_t)(32 * b0 - P0);
-    const int32_t Ms = b0 - 1;
-    const uint32_t p = (uint32_t)Ms & 1u;
-    const int32_t es = 8 + 2 * (Ms >> 1);
-    // the wave's range starts at lane 0's first dword
-    const int32_t P00 = c0w * cb;
-    const int32_t es0 = 8 + 2 * ((((P00 + 31) >> 5) - 1) >> 1);
-    const uint32_t ulo = (uint32_t)es0 >> 2;
-    __builtin_amdgcn_wave_barrier();
-    // four rounds of 64 units (the wave needs <= 252 for cb <= 31), batched:
-    // every table entry first, one uniform choice of the unit decoder, then
-    // the reads
-    uint32_t uu[4], wc[4];
-    uint2 te[4];
-    bool gen = false;
+  for (int r = 0; r < 4; r++) {
+    uu[r] = ulo + 64 * r + l;
+    const uint32_t wu = uu[r] >> W.wsh;
+    wc[r] = wu < W.wlast ? wu : W.wlast;
+    te[r] = L.TAB[wc[r]];
+    gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
+  }
+  v4u dv[4];
+  if (__builtin_amdgcn_ballot_w64(gen) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
+  } else {
+    // (rare: one unit at a time, so the general decoder's temporaries do
+    // not set the kernel's register count)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      uu[r] = ulo + 64 * r + l;
-      const uint32_t wu = uu[r] >> W.wsh;
-      wc[r] = wu < W.wlast ? wu : W.wlast;
-      te[r] = L.TAB[wc[r]];
-      gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
+      dv[r] = bwr_unit_te<SGN>(L, W, uu[r], wc[r], te[r]);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    v4u dv[4];
-    if (__builtin_amdgcn_ballot_w64(gen) == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
-    } else {
-      // (rare: one unit at a time, so the general decoder's temporaries do
-      // not set the kernel's register count)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        dv[r] = bwr_unit_te<SGN>(L, W, uu[r], wc[r], te[r]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) *(v4u*)(wsp + 4 * (64 * r + l)) = dv[r];
-    __builtin_amdgcn_wave_barrier();
-    pc.mark(11);
-    const uint32_t g = (uint32_t)es - 4 * ulo;
-    const bool first = k == 0 && w == 0 && l == 0;
-    uint32_t A = 0, B = 0;
-    dd_codes_at<CB>(wsp, g, p, n, first, x0, x1, xl[k], A, B);
-    __builtin_amdgcn_wave_barrier();
-    pc.mark(12);
-    // inclusive wave scan of the (A, B) aggregates, 16 codes per lane
-    const uint32_t As = A, Bs = B;
-    scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
-    scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
-    scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
-    scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
-    scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
-    scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
-    // fold the lane's exclusive wave prefix (Ae, Be) into its values now:
-    // x_i = Xs + (16 l + i + 1) Ds + [Be + (i + 1) Ae + xl_i], with (Xs, Ds)
-    // the state at the start of the (plane, wave) block
-    {
-      const uint32_t ae = A - As, be = B - Bs - 16 * (A - As);
-      uint32_t t = be;
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        t += ae;
-        xl[k][i] += t;
-      }
-    }
-    if (l == 63) {
-      L.red[k][w][0] = A;
-      L.red[k][w][1] = B;
-    }
-    pc.mark(13);
   }
+#pragma unroll
+  for (int r = 0; r < 4; r++) *(v4u*)(wsp + 4 * (64 * r + l)) = dv[r];
+  __builtin_amdgcn_wave_barrier();
+  pc.mark(11);
+  const uint32_t g = (uint32_t)es - 4 * ulo;
+  const bool first = K == 0 && w == 0 && l == 0;
+  uint32_t A = 0, B = 0;
+  dd_codes_at<CB>(wsp, g, p, n, first, x0, x1, xk, A, B);
+  __builtin_amdgcn_wave_barrier();
+  pc.mark(12);
+  // inclusive wave scan of the (A, B) aggregates, 16 codes per lane
+  const uint32_t As = A, Bs = B;
+  scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
+  scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
+  scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
+  scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
+  scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
+  scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
+  // the lane's exclusive wave prefix: x_i = Xs + (16 l + i + 1) Ds + be +
+  // (i + 1) ae + xk_i, with (Xs, Ds) the state at the start of the (plane,
+  // wave) block
+  ae = A - As;
+  be = B - Bs - 16 * (A - As);
+  if (l == 63) {
+    L.red[K][w][0] = A;
+    L.red[K][w][1] = B;
+  }
+  pc.mark(13);
+}
+
+// After plane K's barrier: the start state of every (K, wave) block from the
+// four wave totals (scalar registers), then the one fold of the lane's
+// prefix and its block's start into its 16 values.  (X, D) = state at the
+// end of plane K - 1 on entry, of plane K on return.
+template <int K>
+__device__ __forceinline__ void plane_fold(const Lds& L, uint32_t w, uint32_t l, uint32_t& X, uint32_t& D,
+                                          uint32_t ae, uint32_t be, uint32_t (&xk)[16]) {
+  uint32_t Xs = 0, Ds = 0;
+#pragma unroll
+  for (int v = 0; v < NWV; v++) {
+    if ((uint32_t)v == w) {
+      Xs = X;
+      Ds = D;
+    }
+    const uint32_t A = __builtin_amdgcn_readfirstlane(L.red[K][v][0]);
+    const uint32_t B = __builtin_amdgcn_readfirstlane(L.red[K][v][1]);
+    X = X + 1024u * D + B;
+    D = D + A;
+  }
+  uint32_t t = Xs + be + 16u * l * Ds;
+  const uint32_t st = Ds + ae;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    t += st;
+    xk[i] += t;
+  }
+}
+
+// The four planes of one tile (code width CB), each followed by one
+// workgroup barrier that publishes the (plane, wave) totals; after the first
+// one the waves' DD-header verdicts are ANDed (vok).  Exactly four barriers
+// whatever the data (the caller's default case executes four too).
+template <int CB, bool SGN>
+__device__ __forceinline__ void planes4(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
+                                        uint32_t (&xl)[4][16], bool& ok, Clock& pc) {
+  uint32_t X = 0, D = 0, ae = 0, be = 0;
+  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae, be, pc);
+  sc::lds_barrier();
+  {
+    uint32_t all = 1;
+#pragma unroll
+    for (int v = 0; v < NWV; v++) all &= L.vok[v];
+    ok = ok && all != 0;
+  }
+  if (ok) plane_fold<0>(L, w, l, X, D, ae, be, xl[0]);
+  plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae, be, pc);
+  sc::lds_barrier();
+  if (ok) plane_fold<1>(L, w, l, X, D, ae, be, xl[1]);
+  plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae, be, pc);
+  sc::lds_barrier();
+  if (ok) plane_fold<2>(L, w, l, X, D, ae, be, xl[2]);
+  plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae, be, pc);
+  sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
+  if (ok) plane_fold<3>(L, w, l, X, D, ae, be, xl[3]);
 }
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
@@ -455,14 +504,18 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       fl = c32(L, b + 12);
       ml = c32(L, b + 16);
       const uint32_t Lb = c32(L, m), nwr = c32(L, m + 4), ws0 = c32(L, m + 13);
-      // lane l: window entries 4l..4l+3 = 36 bytes at e0 (e0 & 3 is uniform)
-      const uint32_t e0 = m + 8 + 36 * l;
+      // Wave w parses windows [64 w, 64 w + 64), lane l window 64 w + l (9
+      // bytes at e0), and writes their table entries with offsets relative
+      // to its part; the part totals go through LDS (B2) and each wave then
+      // adds its part's prefix to its own entries (B2b).
+      const uint32_t wi = 64 * w + l;
+      const uint32_t e0 = m + 8 + 9 * wi;
       const uint32_t* rp = L.C + (e0 >> 2);
-      uint32_t R[10], E[9];
-#pragma unroll
-      for (int k = 0; k < 10; k++) R[k] = rp[k];
-#pragma unroll
-      for (int k = 0; k < 9; k++) E[k] = __builtin_amdgcn_alignbyte(R[k + 1], R[k], e0 & 3);
+      const uint32_t R0 = rp[0], R1 = rp[1], R2 = rp[2], R3 = rp[3];
+      const uint32_t vmin = __builtin_amdgcn_alignbyte(R1, R0, e0 & 3);
+      const uint32_t E1 = __builtin_amdgcn_alignbyte(R2, R1, e0 & 3);
+      const uint32_t E2 = __builtin_amdgcn_alignbyte(R3, R2, e0 & 3);
+      const uint32_t bits = E1 & 0xffu, nb = __builtin_amdgcn_alignbyte(E2, E1, 1);
       nwin = nwr < TABN ? nwr : TABN;
       const uint32_t f = m + 8 + 9 * nwin;
       const uint32_t d0 = c32(L, f), d1 = c32(L, f + 4), d2 = c32(L, f + 8), d3 = c32(L, f + 12),
@@ -475,55 +528,41 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
            (Lb - 1) / ws + 1 == nwin;
       wsh = ok ? 31 - __builtin_clz(ws) - 4 : 0;
       if (ok) {
-        // every wave reads all window headers, so all waves reach the same
-        // verdict and offsets without a barrier
-        uint32_t cs[4], kind[4], mn[4];
-        bool bad = false;
-        auto byte_at = [&](int o) -> uint32_t { return (E[o >> 2] >> (8 * (o & 3))) & 0xffu; };
-        auto dw_at = [&](int o) -> uint32_t {
-          return (o & 3) ? __builtin_amdgcn_alignbyte(E[(o >> 2) + 1], E[o >> 2], o & 3) : E[o >> 2];
-        };
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t wi = 4 * l + q;
-          const uint32_t vmin = dw_at(9 * q), bits = byte_at(9 * q + 4), nb = dw_at(9 * q + 5);
-          const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
-          const bool in = wi < nwin;
-          bad |= in && nb != want;
-          const bool raw = bits >= 32 || (nb & 3) != 0;
-          bad |= in && !raw && bits != 8 && bits != 16;
-          kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
-          cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
-          mn[q] = raw ? 0 : vmin;
-        }
-        const uint32_t s4 = cs[0] + cs[1] + cs[2] + cs[3];
-        const uint32_t inc = wave_incscan_u32(s4);
-        const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-        ok = !__builtin_amdgcn_ballot_w64(bad) && total == fl;
-        if (ok && (l >> 4) == w) {
-          uint32_t off = dst + inc - s4;
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            L.TAB[4 * l + q] = make_uint2(off | (kind[q] << 16), mn[q]);
-            off += cs[q];
-          }
-        }
+        const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+        const bool in = wi < nwin;
+        const bool raw = bits >= 32 || (nb & 3) != 0;
+        const bool bad = in && (nb != want || (!raw && bits != 8 && bits != 16));
+        const uint32_t kind = raw ? 2 : bits == 8 ? 0 : 1;
+        const uint32_t cs = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+        const uint32_t inc = wave_incscan_u32(cs);
+        ok = !__builtin_amdgcn_ballot_w64(bad);
+        if (in) L.TAB[wi] = make_uint2((inc - cs) | (kind << 16), raw ? 0 : vmin);
+        if (l == 63) L.wt[w] = inc;
       }
     }
     pc.mark(9);
     // Barrier reachability is uniform by construction: every workgroup
     // barrier below depends only on cur_dma (a function of readlane'd
     // descriptors); the data-dependent verdicts are published through LDS
-    // and read back after a barrier.  Every wave computed `ok` from the same
-    // bytes, so they agree anyway; every wave takes the AND of all of them.
+    // and read back after a barrier, every wave taking the AND of all.
     if (l == 0) L.vd[w] = ok ? 1u : 0u;
-    lds_barrier();  // B2: window table + header verdicts
+    lds_barrier();  // B2: part tables, part totals, header verdicts
     {
-      uint32_t all = 1;
+      uint32_t all = 1, tot = 0, pre = dst;
 #pragma unroll
-      for (int v = 0; v < NWV; v++) all &= L.vd[v];
-      ok = ok && all != 0;
+      for (int v = 0; v < NWV; v++) {
+        all &= L.vd[v];
+        const uint32_t t = __builtin_amdgcn_readfirstlane(L.wt[v]);
+        if ((uint32_t)v < w) pre += t;
+        tot += t;
+      }
+      ok = ok && all != 0 && tot == fl;
+      // each wave makes its own entries absolute (image offset of the
+      // window's compressed data)
+      const uint32_t wi = 64 * w + l;
+      if (ok && wi < nwin) L.TAB[wi].x += pre;
     }
+    lds_barrier();  // B2b: the window table
     if (!ok) {
       wsh = 0;
       nwin = 1;
@@ -549,29 +588,34 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
            num1lo == NV && num1hi == 0 && comp1 == 17 + 8 * words;
     }
     pc.mark(10);
-    if (ok) {
-      // ---- four planes: BWR⁻¹ into the wave scratch, codes, local scans ---
-      // one instantiation per code width: the plane loop unrolls and every
-      // plane's codes land directly in their value registers
-      switch (cb) {
-#define TDBG_CB(c) \
-  case c: planes<c, SGN>(L, W, w, l, x0, x1, xl, pc); break;
-        TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
-        TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
-        TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
-        TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
-        TDBG_CB(31)
-#undef TDBG_CB
-        default: break;
-      }
-    }
+    // ---- four planes: BWR⁻¹ into the wave scratch, codes, wave scan; one
+    // barrier per plane publishes the (plane, wave) totals, and the lane's
+    // prefix and its block's start fold into its values in one pass -----
     if (l == 0) L.vok[w] = ok ? 1u : 0u;
-    lds_barrier();  // B3: C and TAB are free, the (plane, wave) totals and verdicts are in LDS
-    {
-      uint32_t all = 1;
+    // one instantiation per code width: the plane loop unrolls and every
+    // plane's codes land directly in their value registers
+    switch (ok ? cb : 0u) {
+#define TDBG_CB(c) \
+  case c: planes4<c, SGN>(L, W, w, l, x0, x1, xl, ok, pc); break;
+      TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
+      TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
+      TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
+      TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
+      TDBG_CB(31)
+#undef TDBG_CB
+      default:  // declined (ok is false): the same four barriers
+        ok = false;
+        // (defined values: an undefined xl here lets the register allocator
+        // keep the last tile's values live around the loop)
 #pragma unroll
-      for (int v = 0; v < NWV; v++) all &= L.vok[v];
-      ok = ok && all != 0;
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+          for (int i = 0; i < 16; i++) xl[k][i] = 0;
+        lds_barrier();
+        lds_barrier();
+        lds_barrier();
+        lds_barrier();
+        break;
     }
     }  // cur_dma
     // tiles bigger than CCAP belong to the raw-DoubleDelta kernel, which runs
@@ -586,31 +630,6 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     const bool nxt_dma = jn < ntl && fits(nxt);
     if (nxt_dma) dma(L, nxt);
     if (ok) {
-      // start state of every (plane, wave) block: 1,024 codes each, in order
-      uint32_t X = 0, D = 0, Xs[4] = {0, 0, 0, 0}, Ds[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int v = 0; v < NWV; v++) {
-          if ((uint32_t)v == w) {
-            Xs[k] = X;
-            Ds[k] = D;
-          }
-          // uniform: scalar registers, not 32 VGPRs of LDS reads
-          const uint32_t A = __builtin_amdgcn_readfirstlane(L.red[k][v][0]);
-          const uint32_t B = __builtin_amdgcn_readfirstlane(L.red[k][v][1]);
-          X = X + 1024u * D + B;
-          D = D + A;
-        }
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint32_t t = Xs[k] + 16u * l * Ds[k];
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          t += Ds[k];
-          xl[k][i] += t;
-        }
-      }
       pc.mark(14);
       // byteshuffle⁻¹: unit i of the lane = dword i of the four planes,
       // transposed bytewise (out dword b byte k = plane k value byte b).
