@@ -137,6 +137,7 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     ctx.time_launches(steps)
     fused0, fb0, _ = ctx.path_stats()
     s0 = ctx.stream_tiles()
+    c0 = ctx.stream_chunks()
     batch.d_status.fill_(-1)
     if dist is not None:
         dist.barrier()
@@ -156,9 +157,11 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
         raise SystemExit(f"timed launches: device status nonzero: {np.unique(st)}")
     fused1, fb1, _ = ctx.path_stats()
     s1 = ctx.stream_tiles()
+    c1 = ctx.stream_chunks()
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, DIST_DEV)
-    return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0, s1 - s0)
+    return (elapsed, float(np.mean(kern_ms)), float(np.mean(total_ms)), fused1 - fused0, fb1 - fb0, s1 - s0,
+            c1 - c0)
 
 
 def time_forward(engine, ctx, dp, vals, idx, pool, steps: int, warmup: int, dist):
@@ -300,7 +303,7 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
             raise SystemExit(f"{cfgname} {var}: first pass status nonzero: {np.unique(st)}")
         if not ablation:
             verify(batch, vals, idx)
-        elapsed, kern_ms, launch_ms, fused, fallback, streamed = time_device(
+        elapsed, kern_ms, launch_ms, fused, fallback, streamed, schunks = time_device(
             engine, ctx, dp, batch, steps, warmup, dist, world)
         if not ablation:
             verify(batch, vals, idx)
@@ -309,6 +312,7 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
         unf_job = sum_over_ranks(dist, unf, DIST_DEV) if dist is not None else unf
         res[var] = dict(elapsed=elapsed, kern_ms=kern_ms, launch_ms=launch_ms, b_alg=b_alg, unf=unf, unf_job=unf_job,
                         out_bytes=int(vals[0].nbytes), fused=fused, fallback=fallback, streamed=streamed,
+                        stream_chunks=schunks,
                         packed=packed, offs=offs, sizes=sizes, steps=steps, ntiles=ntiles)
         if forward and vi == 0 and not ablation and cfgname != "fscale":  # (lossy: values differ)
             res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, steps, warmup, dist)
@@ -331,6 +335,9 @@ def frac(r):
 
 
 def kernel_name(cfgname, r):
+    if cfgname == "c5big" and r.get("stream_chunks"):
+        return ("chunk directory (dir_count/dir_scan/dir_fill) + unfilter_stream_kernel + unfilter_stream_raw_kernel "
+                "on chunk records + unfilter_fused_kernel (queue of declined chunks)")
     if cfgname in ("c5", "c5big") and r["streamed"]:
         return ("unfilter_stream_kernel + unfilter_stream_raw_kernel + unfilter_fused_kernel (queue of "
                 "declined tiles)")
@@ -364,23 +371,45 @@ def variant_line(cfgname, var, r, world):
     return {"GiBps": round(gibps(r, world), 2), "roofline_frac": round(frac(r), 4),
             "kernel_ms": round(r["kern_ms"], 4), "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 4),
             "fallback_tiles_timed": r["fallback"], "stream_tiles_timed": r["streamed"],
+            "stream_chunks_timed": r.get("stream_chunks", 0),
             "algorithmic_bytes_per_launch": int(r["b_alg"]),
             "traffic": load_traffic(cfgname, var)}
 
 
-def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048):
+def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, scaling=False):
     cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
                                 ntiles_sample, threads, seconds)
-    return {
+    line = {
         "value": round(cpu, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{ntl} {cfgname.upper()} '{var}' tiles ({min(ntiles_sample, r['offs'].size)}-tile sample, "
                   f"repeated) in {el:.2f}s on {threads} threads of '{cpu_model()}' ({os.cpu_count()} CPUs "
-                  "visible; 16 threads = one GPU's share of the box), tdbg_unfilter_tiles_cpu (the C-ABI's "
-                  "C++ CPU entry, the reference's tile x chunk-range split)",
+                  f"visible, {len(os.sched_getaffinity(0))} in this process's affinity; 16 threads = one GPU's "
+                  "share of the box), tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry, the reference's "
+                  "tile x chunk-range split)",
     }
+    if scaling:
+        # per-thread rate and the thread-scaling curve of the same sample, so
+        # the all-cores figure can be read off (the box lends a GPU job 16
+        # threads; running on all of them is not allowed there)
+        curve = {}
+        for t in (1, 2, 4, 8):
+            if t < threads:
+                v, _, _ = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
+                                       min(ntiles_sample, 256 * t), t, max(1.0, seconds / 5))
+                curve[str(t)] = round(v, 3)
+        curve[str(threads)] = round(cpu, 3)
+        line["thread_scaling_GiBps"] = curve
+        if "1" in curve:
+            ncpu = os.cpu_count() or threads
+            line["per_thread_GiBps"] = curve["1"]
+            line["all_cores_linear_estimate_GiBps"] = {
+                "cores": ncpu, "value": round(min(curve["1"] * ncpu, cpu * ncpu / threads), 1),
+                "note": "not measured: min(1-thread rate x cores, measured rate x cores / threads); "
+                        "memory bandwidth would cap it lower"}
+    return line
 
 
 # the other BASELINE configs timed in the default (N = 1) run, per-GPU sizes
@@ -419,6 +448,7 @@ def headline_line(args, W, variants, res, world):
             "fused_tiles_timed": r["fused"],
             "fallback_tiles_timed": r["fallback"],
             "stream_tiles_timed": r["streamed"],
+            "stream_chunks_timed": r.get("stream_chunks", 0),
         },
         "roofline": roofline(args.config, head, r),
     }
@@ -570,7 +600,7 @@ def main():
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sh.values()), 4)}
     if rank == 0 and not args.no_cpu_baseline:
         # after every timed region, at any N (rank 0 only)
-        line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds, scaling=True)
     if rank == 0:
         print(json.dumps(line))
     if dist is not None:

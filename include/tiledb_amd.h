@@ -329,6 +329,12 @@ int tdbg_context_stream_stats(const tdbg_context* ctx, uint64_t* stream_tiles);
 /* Of those, the tiles the raw-DoubleDelta streaming kernel took (C5 tiles
  * whose DD stage stored the values raw, tdbg_stream_raw.hip). */
 int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles);
+/* Chunk-parallel launches (TDBG_CHUNK_PARALLEL, or fewer tiles than CUs) of
+ * the headline pipeline: the chunks the streaming kernels took from the
+ * device chunk directory (each a 64 KiB chunk of a multi-chunk tile, decoded
+ * as the one-chunk tiles are).  Cumulative; waits for the context's last
+ * launch. */
+int tdbg_context_stream_chunk_stats(const tdbg_context* c, uint64_t* chunks);
 /* Forward direction: tiles the LDS-resident kernel for [BYTESHUFFLE,
  * DOUBLE_DELTA, BWR(256)] on INT32 / UINT32 64 KiB tiles filtered
  * (tdbg_forward_stream.hip; the others run on the general forward kernel).
@@ -451,6 +457,70 @@ int tdbg_dense_read_host(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t nti
                          const uint64_t* in_size, const int64_t* tile_start, const tdbg_dense_copy_config* cfg,
                          uint8_t* result, uint64_t result_size, uint32_t flags, int32_t* host_status,
                          uint64_t batch_bytes);
+
+/* ---- dense reads with several fragments, fill values, var-sized cells -----
+ * DenseReader::copy_fixed_tiles / copy_offset_tiles / fix_offsets_buffer /
+ * copy_var_tiles (dense_reader.cc:1199-1236, 1521-2000).  Space tile t has
+ * one unfiltered tile per fragment fd (pointer arrays of ntiles * nfrag
+ * entries, [t * nfrag + fd]; NULL: the fragment has no tile there); fragment
+ * fd covers the inclusive domain d_frag_dom[(fd * dim_num + d) * 2 + {0, 1}].
+ * Where domains overlap, the fragment with the LOWER index wins (the
+ * reference walks them from the last to the first, each overwriting); cells
+ * no fragment covers get the fill value (Attribute::fill_value) and
+ * fill_validity.  Result buffers are in the query layout (base.layout). */
+typedef struct tdbg_dense_frag_config {
+  tdbg_dense_copy_config base; /* dims, subarray, tile extents, cell/result order;
+                                  base.cell_size: bytes per cell (fixed), 8 (var) */
+  uint32_t nfrag;              /* fragments (0: every cell gets the fill value) */
+  uint32_t nullable;           /* copy validity tiles (1 byte per cell) too */
+  uint32_t fill_size;          /* bytes of the fill value (fixed: == cell_size) */
+  uint32_t fill_validity;      /* Attribute::fill_value_validity (0 or 1) */
+  uint32_t elements_mode;      /* var: offsets count elements of data_type_size (elements_mode_) */
+  uint32_t data_type_size;     /* var: datatype_size of the attribute */
+} tdbg_dense_frag_config;
+
+/* Fixed-size cells: device tiles / validity tiles / fill value -> device
+ * result (+ validity). */
+int tdbg_dense_copy_fragments_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
+                                    const int64_t* d_tile_start, const int64_t* d_frag_dom,
+                                    const uint8_t* const* d_tiles, const uint8_t* const* d_validity,
+                                    const uint8_t* d_fill_value, uint8_t* d_result, uint8_t* d_result_validity,
+                                    tdbg_stream stream);
+
+/* Var-sized cells, step 1 (copy_offset_tiles + fix_offsets_buffer): from the
+ * unfiltered offsets tiles (uint64, tile cells + 1 entries: the extra offset
+ * of tile.h:144-146 included) and var tiles, the result offsets (uint64, one
+ * per result cell, in elements in elements mode) and their total
+ * (*d_var_total, device); the cells' source addresses stay in ctx for step 2. */
+int tdbg_dense_var_offsets_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
+                                 const int64_t* d_tile_start, const int64_t* d_frag_dom,
+                                 const uint8_t* const* d_offset_tiles, const uint8_t* const* d_var_tiles,
+                                 const uint8_t* const* d_validity, const uint8_t* d_fill_value,
+                                 uint64_t* d_result_offsets, uint8_t* d_result_validity, uint64_t* d_var_total,
+                                 tdbg_stream stream);
+/* Step 2 (copy_var_tiles): every cell's bytes to d_result_var + offset (x the
+ * type size in elements mode); d_result_var holds *d_var_total units. */
+int tdbg_dense_var_copy_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg,
+                              const uint64_t* d_result_offsets, const uint64_t* d_var_total, uint8_t* d_result_var,
+                              tdbg_stream stream);
+
+/* Host-resident var-sized dense read fused with the transfers: the filtered
+ * offsets and var tiles of every (space tile, fragment) -> H2D -> unfilter
+ * (offsets tiles as TDBG_TILE_OFFSETS with the extra offset = the var tile's
+ * unfiltered size, reader_base.cc:885-893) -> steps 1 and 2 -> D2H of the
+ * result offsets (ncells uint64) and var bytes.  var_unfiltered_size[i]: the
+ * var tile's unfiltered bytes; NULL filtered pointers: fragment absent.
+ * *var_total receives the var bytes; TDBG_E_OUT_FULL if var_cap is smaller
+ * (nothing copied to result_var).  Statuses per (tile, fragment) pair: the
+ * offsets tile's, or the var tile's if that one failed.  cfg->nullable must
+ * be 0 here (validity tiles: tdbg_dense_var_offsets_async). */
+int tdbg_dense_read_var_host(tdbg_context* ctx, const tdbg_pipeline* p_offsets, const tdbg_pipeline* p_var,
+                             const tdbg_dense_frag_config* cfg, uint64_t ntiles, const int64_t* tile_start,
+                             const int64_t* frag_dom, const uint8_t* const* off_filtered,
+                             const uint64_t* off_filtered_size, const uint8_t* const* var_filtered,
+                             const uint64_t* var_filtered_size, const uint64_t* var_unfiltered_size,
+                             const uint8_t* fill_value, uint64_t* result_offsets, uint8_t* result_var,
+                             uint64_t var_cap, uint64_t* var_total, int32_t* host_status);
 
 #ifdef __cplusplus
 }

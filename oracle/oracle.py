@@ -267,3 +267,169 @@ def dense_subarray_cells(tiles, tile_start, tile_extent, cell_size: int, sub_lo,
     if layout == 1:
         out = np.transpose(out, tuple(reversed(range(nd))) + (nd,))
     return np.ascontiguousarray(out).reshape(-1)
+
+
+def _tile_cells(raw, ext, cell_size: int, cell_order: int):
+    """A tile's cells as an array indexed by (coords..., byte): cell order 0
+    row-major (last dimension fastest), 1 col-major."""
+    nd = len(ext)
+    cells = np.frombuffer(bytes(raw), dtype=np.uint8)[: int(np.prod(ext)) * cell_size].reshape(-1, cell_size)
+    blk = cells.reshape((tuple(ext) if cell_order == 0 else tuple(reversed(ext))) + (cell_size,))
+    if cell_order == 1:
+        blk = np.transpose(blk, tuple(reversed(range(nd))) + (nd,))
+    return blk
+
+
+def _frag_masks(t_start, ext, lo, hi, frag_dom, present):
+    """Per space tile: the region (tile box intersected with the subarray, as
+    slices on both sides) and, for every fragment domain fd, the cells of the
+    region it covers (cell_slab_overlaps_range, dense_reader.cc:1521-1552: a
+    cell of a slab overlaps a fragment domain iff every coordinate lies in it)
+    -- False where the fragment has no tile here (tile_tuples[fd] == nullptr)."""
+    nd = len(ext)
+    a = [max(t_start[d], lo[d]) for d in range(nd)]
+    b = [min(t_start[d] + ext[d] - 1, hi[d]) for d in range(nd)]
+    if any(b[d] < a[d] for d in range(nd)):
+        return None
+    src = tuple(slice(a[d] - t_start[d], b[d] - t_start[d] + 1) for d in range(nd))
+    dst = tuple(slice(a[d] - lo[d], b[d] - lo[d] + 1) for d in range(nd))
+    grids = np.meshgrid(*[np.arange(a[d], b[d] + 1) for d in range(nd)], indexing="ij")
+    masks = []
+    for fd, dom in enumerate(frag_dom):
+        m = np.ones(grids[0].shape, dtype=bool) if present[fd] else np.zeros(grids[0].shape, dtype=bool)
+        for d in range(nd):
+            m &= (grids[d] >= dom[d][0]) & (grids[d] <= dom[d][1])
+        masks.append(m)
+    return src, dst, masks
+
+
+def dense_copy_fragments(tiles, tile_start, tile_extent, cell_size: int, sub_lo, sub_hi, frag_dom, fill_value,
+                         cell_order: int = 0, layout: int = 0, validity=None, fill_validity: int = 0):
+    """DenseReader::copy_fixed_tiles (dense_reader.cc:1555-1750) with several
+    fragments: tiles[t][fd] is fragment fd's unfiltered tile of space tile t
+    (None: no tile), frag_dom[fd] its domain ((lo, hi) per dimension).  The
+    reference walks the fragment domains from the last to the first, each
+    copying the cells it overlaps over what the later ones wrote
+    (:1600-1660), and fills the cells the last domain does not write with the
+    fill value (:1676-1702), or the whole slab when there is no fragment
+    (:1708-1719).  Returns the result bytes (and validity bytes when
+    `validity` holds per-(t, fd) validity tiles)."""
+    nd = len(tile_extent)
+    ext = [int(e) for e in tile_extent]
+    lo = [int(x) for x in sub_lo]
+    hi = [int(x) for x in sub_hi]
+    shape = tuple(h - l + 1 for l, h in zip(lo, hi))
+    fill = np.frombuffer(bytes(fill_value), dtype=np.uint8)
+    assert fill.size == cell_size
+    out = np.zeros(shape + (cell_size,), dtype=np.uint8)
+    outv = np.zeros(shape, dtype=np.uint8)
+    F = len(frag_dom)
+    for t in range(len(tiles)):
+        s = [int(x) for x in tile_start[t]]
+        present = [tiles[t][fd] is not None for fd in range(F)]
+        r = _frag_masks(s, ext, lo, hi, frag_dom, present)
+        if r is None:
+            continue
+        src, dst, masks = r
+        reg = out[dst]
+        regv = outv[dst]
+        if F == 0:
+            reg[...] = fill
+            regv[...] = fill_validity
+        for fd in range(F - 1, -1, -1):
+            m = masks[fd]
+            if present[fd]:
+                reg[m] = _tile_cells(tiles[t][fd], ext, cell_size, cell_order)[src][m]
+                if validity is not None:
+                    regv[m] = _tile_cells(validity[t][fd], ext, 1, cell_order)[src][..., 0][m]
+            if fd == F - 1:
+                reg[~m] = fill
+                regv[~m] = fill_validity
+        out[dst] = reg
+        outv[dst] = regv
+    if layout == 1:
+        out = np.transpose(out, tuple(reversed(range(nd))) + (nd,))
+        outv = np.transpose(outv, tuple(reversed(range(nd))))
+    res = np.ascontiguousarray(out).reshape(-1)
+    return (res, np.ascontiguousarray(outv).reshape(-1)) if validity is not None else res
+
+
+def dense_var_read(off_tiles, var_tiles, tile_start, tile_extent, sub_lo, sub_hi, frag_dom, fill_value,
+                   cell_order: int = 0, layout: int = 0, elements_mode: bool = False, type_size: int = 1):
+    """The dense read of a var-sized attribute with several fragments:
+    DenseReader::copy_offset_tiles (dense_reader.cc:1753-1926) writes each
+    result cell's size (offsets tile entries i + 1 - i, of the unfiltered
+    offsets tile with its extra offset, tile.h:144-146; divided by the type
+    size in elements mode) and the address of its bytes in the var tile, or
+    the max sentinel for cells no fragment writes; fix_offsets_buffer
+    (:1199-1236) turns the sizes into offsets (a sentinel becomes the fill
+    value's size and the fill value's bytes); copy_var_tiles (:1929-2000)
+    copies each cell's bytes to its offset (times the type size in elements
+    mode).  off_tiles[t][fd] / var_tiles[t][fd]: fragment fd's unfiltered
+    offsets tile (uint64, cells + 1 entries) and var tile of space tile t.
+    Returns (offsets as uint64 in result order, var bytes)."""
+    nd = len(tile_extent)
+    ext = [int(e) for e in tile_extent]
+    lo = [int(x) for x in sub_lo]
+    hi = [int(x) for x in sub_hi]
+    shape = tuple(h - l + 1 for l, h in zip(lo, hi))
+    F = len(frag_dom)
+    SENT = (1 << 64) - 1
+    size = np.full(shape, SENT, dtype=np.uint64)
+    ref_t = np.full(shape, -1, dtype=np.int64)   # (t, fd, var byte offset) of each cell's bytes
+    ref_f = np.full(shape, -1, dtype=np.int64)
+    ref_o = np.zeros(shape, dtype=np.uint64)
+    div = type_size if elements_mode else 1
+    for t in range(len(off_tiles)):
+        s = [int(x) for x in tile_start[t]]
+        present = [off_tiles[t][fd] is not None for fd in range(F)]
+        r = _frag_masks(s, ext, lo, hi, frag_dom, present)
+        if r is None:
+            continue
+        src, dst, masks = r
+        for fd in range(F - 1, -1, -1):
+            m = masks[fd]
+            if present[fd]:
+                offs = np.frombuffer(bytes(off_tiles[t][fd]), dtype=np.uint64)
+                ncell = int(np.prod(ext))
+                pos = np.arange(ncell, dtype=np.int64).reshape(tuple(ext) if cell_order == 0 else tuple(reversed(ext)))
+                if cell_order == 1:
+                    pos = np.transpose(pos)
+                p = pos[src]
+                sz = (offs[p + 1] - offs[p]) // np.uint64(div)
+                size[dst][m] = sz[m]
+                ref_t[dst][m] = t
+                ref_f[dst][m] = fd
+                ref_o[dst][m] = offs[p][m]
+            if fd == F - 1:
+                size[dst][~m] = SENT
+                ref_t[dst][~m] = -1
+        if F == 0:
+            size[dst] = SENT
+            ref_t[dst] = -1
+    if layout == 1:
+        size, ref_t, ref_f, ref_o = (np.transpose(x) for x in (size, ref_t, ref_f, ref_o))
+    size, ref_t, ref_f, ref_o = (np.ascontiguousarray(x).reshape(-1) for x in (size, ref_t, ref_f, ref_o))
+    fill = bytes(fill_value)
+    fill_sz = len(fill) // type_size if elements_mode else len(fill)
+    offsets = np.zeros(size.size, dtype=np.uint64)
+    total = 0
+    for i in range(size.size):  # fix_offsets_buffer
+        v = int(size[i])
+        if v == SENT:
+            v = fill_sz
+            ref_t[i] = -1
+        offsets[i] = total
+        total += v
+    mult = type_size if elements_mode else 1
+    data = bytearray(total * mult)
+    for i in range(size.size):  # copy_var_tiles
+        o = int(offsets[i]) * mult
+        n = (int(offsets[i + 1]) if i + 1 < size.size else total) * mult - o
+        if ref_t[i] < 0:
+            data[o:o + n] = fill[:n]
+        else:
+            vt = bytes(var_tiles[int(ref_t[i])][int(ref_f[i])])
+            b = int(ref_o[i])
+            data[o:o + n] = vt[b:b + n]
+    return offsets, bytes(data)

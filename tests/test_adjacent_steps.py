@@ -274,3 +274,195 @@ def test_dense_copy_async_skips_failed_tiles(oracle_mod):
     assert mask.any() and not mask.all()
     assert np.array_equal(got[~mask], want[~mask])
     assert (got[mask] == 7).all()
+
+
+# ---------------------------------------------------------------------------
+# Several fragments, fill values, var-sized cells (dense_reader.cc:1199-2000)
+# ---------------------------------------------------------------------------
+def _frag_layout(rng, shape_tiles, ext, nfrag):
+    """Fragment domains (random boxes over the array, overlapping) and, per
+    (space tile, fragment), whether the fragment has a tile there (it must
+    when its domain meets the tile; a few that do not meet it get one too)."""
+    nd = len(ext)
+    full = [t * e for t, e in zip(shape_tiles, ext)]
+    doms = []
+    for _ in range(nfrag):
+        lo = [int(rng.integers(0, full[d])) for d in range(nd)]
+        hi = [int(rng.integers(lo[d], full[d])) for d in range(nd)]
+        doms.append([(lo[d], hi[d]) for d in range(nd)])
+    starts = [tuple(i * e for i, e in zip(idx, ext)) for idx in np.ndindex(*shape_tiles)]
+    present = []
+    for s in starts:
+        row = []
+        for dom in doms:
+            meets = all(dom[d][0] <= s[d] + ext[d] - 1 and dom[d][1] >= s[d] for d in range(nd))
+            row.append(meets or bool(rng.integers(0, 4) == 0))
+        present.append(row)
+    return doms, np.array(starts, dtype=np.int64), present
+
+
+def test_oracle_dense_var_single_fragment_is_concatenation(oracle_mod):
+    """The var restatement with one fragment covering the subarray and whole
+    tiles equals the cells' bytes in result order (no fill involved)."""
+    rng = np.random.default_rng(3)
+    ext = (4, 6)
+    starts = [(0, 0), (0, 6), (4, 0), (4, 6)]
+    cells, offs_t, var_t = {}, [], []
+    for s in starts:
+        lens = rng.integers(0, 9, 24)
+        blob, offs = b"", []
+        for k in range(24):
+            r, c = divmod(k, 6)
+            b = bytes(rng.integers(0, 256, int(lens[k]), dtype=np.uint8))
+            cells[(s[0] + r, s[1] + c)] = b
+            offs.append(len(blob))
+            blob += b
+        offs_t.append([np.array(offs + [len(blob)], dtype=np.uint64).tobytes()])
+        var_t.append([blob])
+    o, data = oracle_mod.dense_var_read(offs_t, var_t, starts, ext, (1, 2), (6, 10), [[(0, 7), (0, 11)]], b"xy")
+    want = [cells[(r, c)] for r in range(1, 7) for c in range(2, 11)]
+    assert data == b"".join(want)
+    assert list(o) == list(np.cumsum([0] + [len(w) for w in want[:-1]]))
+
+
+_FRAGS = [((3, 4), (8, 16), (2, 3), (21, 60), 3, 0, 0, False),
+          ((3, 4), (8, 16), (0, 0), (23, 63), 2, 1, 0, True),
+          ((3, 4), (8, 16), (5, 9), (20, 50), 4, 0, 1, True),
+          ((2, 2, 3), (4, 8, 8), (1, 0, 3), (7, 14, 20), 3, 1, 1, False),
+          ((5,), (512,), (100,), (2400,), 0, 0, 0, True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _FRAGS, ids=lambda c: f"f{c[4]}_t{'x'.join(map(str, c[0]))}_o{c[5]}l{c[6]}")
+def test_dense_copy_fragments(oracle_mod, case):
+    """copy_fixed_tiles with several overlapping fragments, absent tiles, the
+    fill value and validity (nullable), on device tiles: bit-exact against
+    the oracle's restatement (dense_reader.cc:1555-1750)."""
+    import torch
+    from tiledb_amd import engine
+    shape_tiles, ext, lo, hi, nfrag, cell_order, layout, nullable = case
+    rng = np.random.default_rng(nfrag * 7 + cell_order + 3 * layout + len(ext))
+    doms, starts, present = _frag_layout(rng, shape_tiles, ext, nfrag)
+    ncell_t = int(np.prod(ext))
+    cs = 8
+    tiles = [[rng.integers(0, 256, ncell_t * cs, dtype=np.uint8) if present[t][f] else None
+              for f in range(nfrag)] for t in range(len(starts))]
+    vtiles = [[rng.integers(0, 2, ncell_t, dtype=np.uint8) if present[t][f] else None for f in range(nfrag)]
+              for t in range(len(starts))]
+    fill = bytes(range(100, 100 + cs))
+    want = oracle_mod.dense_copy_fragments(tiles, starts, ext, cs, lo, hi, doms, fill, cell_order, layout,
+                                           validity=vtiles if nullable else None, fill_validity=1)
+    dev = torch.device("cuda", 0)
+    keep = []
+
+    def dptr(a):
+        if a is None:
+            return 0
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        keep.append(t)
+        return t.data_ptr()
+
+    tp = torch.from_numpy(np.array([dptr(tiles[t][f]) for t in range(len(starts)) for f in range(nfrag)] or [0],
+                                   dtype=np.uint64).view(np.int64)).to(dev)
+    vp = torch.from_numpy(np.array([dptr(vtiles[t][f]) for t in range(len(starts)) for f in range(nfrag)] or [0],
+                                   dtype=np.uint64).view(np.int64)).to(dev)
+    d_start = torch.from_numpy(starts.reshape(-1)).to(dev)
+    d_dom = torch.from_numpy(np.array(doms, dtype=np.int64).reshape(-1) if nfrag else np.zeros(1, np.int64)).to(dev)
+    d_fill = torch.from_numpy(np.frombuffer(fill, dtype=np.uint8).copy()).to(dev)
+    fc = engine.dense_frag_config(cs, ext, lo, hi, nfrag, cs, cell_order, layout, nullable=nullable, fill_validity=1)
+    ncell = int(np.prod([h - l + 1 for l, h in zip(lo, hi)]))
+    d_res = torch.full((ncell * cs,), 0xEE, dtype=torch.uint8, device=dev)
+    d_resv = torch.full((ncell,), 0xEE, dtype=torch.uint8, device=dev)
+    ctx = engine.Context(0)
+    engine.dense_copy_fragments_async(ctx, fc, len(starts), d_start.data_ptr(), d_dom.data_ptr(), tp.data_ptr(),
+                                      d_fill.data_ptr(), d_res.data_ptr(), vp.data_ptr() if nullable else None,
+                                      d_resv.data_ptr() if nullable else None)
+    torch.cuda.synchronize()
+    if nullable:
+        res, val = want
+        assert np.array_equal(d_res.cpu().numpy(), res)
+        assert np.array_equal(d_resv.cpu().numpy(), val)
+    else:
+        assert np.array_equal(d_res.cpu().numpy(), want)
+
+
+def _var_tiles(rng, ncell_t, maxlen):
+    """One var tile: cells of 0..maxlen bytes; its offsets tile as TileDB
+    writes it (cell byte offsets, no extra offset) and the unfiltered offsets
+    tile with the extra offset (tile.h:144-146)."""
+    lens = rng.integers(0, maxlen + 1, ncell_t)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    var = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    return offs[:-1].copy(), offs, var
+
+
+_VAR = [((3, 4), (8, 16), (2, 3), (21, 60), 3, 0, 0, False),
+        ((3, 4), (8, 16), (0, 0), (23, 63), 1, 1, 0, False),
+        ((2, 2, 3), (4, 8, 8), (1, 0, 3), (7, 14, 20), 3, 1, 1, True),
+        ((5,), (512,), (100,), (2400,), 2, 0, 0, True),
+        ((3, 4), (8, 16), (5, 9), (20, 50), 0, 0, 1, False)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _VAR, ids=lambda c: f"f{c[4]}_t{'x'.join(map(str, c[0]))}_o{c[5]}l{c[6]}_e{int(c[7])}")
+def test_dense_read_var_host(oracle_mod, case):
+    """A var-sized attribute's dense read (copy_offset_tiles +
+    fix_offsets_buffer + copy_var_tiles) from FILTERED offsets and var tiles
+    of several fragments: offsets unfiltered with the extra offset fused on
+    the device, the var bytes gathered there, one D2H of each result buffer;
+    bit-exact against the oracle's restatement, elements mode included."""
+    import torch
+    assert torch.cuda.is_available()
+    from tiledb_amd import engine
+    from tiledb_amd.filter_pipeline import (BitshuffleFilter, BitWidthReductionFilter, PositiveDeltaFilter)
+    shape_tiles, ext, lo, hi, nfrag, cell_order, layout, elements = case
+    tsz = 4 if elements else 1  # elements mode: INT32 cells counted in elements
+    rng = np.random.default_rng(nfrag * 13 + cell_order + 5 * layout + len(ext))
+    doms, starts, present = _frag_layout(rng, shape_tiles, ext, nfrag) if nfrag else \
+        ([], np.array([tuple(i * e for i, e in zip(idx, ext)) for idx in np.ndindex(*shape_tiles)]), [[]] * int(np.prod(shape_tiles)))
+    ncell_t = int(np.prod(ext))
+    offp = FilterPipeline(65536, [PositiveDeltaFilter(1024), BitWidthReductionFilter(256)])
+    varp = FilterPipeline(65536, [BitshuffleFilter()])
+    oo = oracle_mod.OraclePipeline(offp.serialize(), 23, int(Datatype.UINT64), 8)
+    vdt = Datatype.INT32 if elements else Datatype.UINT8
+    ov = oracle_mod.OraclePipeline(varp.serialize(), 23, int(vdt), 4 if elements else 1)
+    off_f, var_f, var_u, off_unf, var_unf = [], [], [], [], []
+    for t in range(len(starts)):
+        ou, vu = [], []
+        for f in range(nfrag):
+            if not present[t][f]:
+                off_f.append(None)
+                var_f.append(None)
+                var_u.append(0)
+                ou.append(None)
+                vu.append(None)
+                continue
+            o_w, o_x, var = _var_tiles(rng, ncell_t, 12)
+            if elements:  # whole INT32 elements per cell
+                o_w, o_x = o_w * 4, o_x * 4
+                var = rng.integers(0, 256, int(o_x[-1]), dtype=np.uint8)
+            off_f.append(np.frombuffer(oo.filter_tile(o_w.view(np.uint8)), dtype=np.uint8))
+            var_f.append(np.frombuffer(ov.filter_tile(var), dtype=np.uint8))
+            var_u.append(var.size)
+            ou.append(o_x.tobytes())
+            vu.append(var.tobytes())
+        off_unf.append(ou)
+        var_unf.append(vu)
+    fill = bytes([7, 8, 9, 10, 11, 12, 13, 14])
+    want_o, want_d = oracle_mod.dense_var_read(off_unf, var_unf, starts, ext, lo, hi, doms, fill, cell_order, layout,
+                                               elements_mode=elements, type_size=tsz)
+    ctx = engine.Context(0)
+    dpo = engine.DevicePipeline(offp.serialize(), 23, int(Datatype.UINT64), 8)
+    dpv = engine.DevicePipeline(varp.serialize(), 23, int(vdt), 4 if elements else 1)
+    fc = engine.dense_frag_config(8, ext, lo, hi, nfrag, len(fill), cell_order, layout, elements_mode=elements,
+                                  data_type_size=tsz)
+    rc, got_o, got_d, st = engine.dense_read_var_host(ctx, dpo, dpv, fc, starts, np.array(doms, dtype=np.int64),
+                                                      off_f, var_f, var_u, fill, len(want_d) + 64)
+    assert rc == 0 and not st.any()
+    assert np.array_equal(got_o, want_o)
+    assert got_d == want_d
+    if len(want_d) > 1:  # a result buffer one byte short: TDBG_E_OUT_FULL, nothing copied
+        with pytest.raises(engine.EngineError) as ei:
+            engine.dense_read_var_host(ctx, dpo, dpv, fc, starts, np.array(doms, dtype=np.int64), off_f, var_f, var_u,
+                                       fill, len(want_d) - 1)
+        assert ei.value.code == 6

@@ -559,3 +559,35 @@ def test_chunk_parallel_corrupt_mix(eng, ctx, oracle_mod):
         if rc == 0:
             o = int(batch.out_off[i])
             assert np.array_equal(out[o:o + osz[i]], ref)
+
+
+@pytest.mark.parametrize("variant", ["active", "ramp", "rand"])
+def test_chunk_stream_multichunk(eng, ctx, oracle_mod, variant):
+    """Multi-chunk C5 tiles (1 MiB minus a few values: 16 chunks, the last
+    one short) in a chunk-parallel launch: the streaming kernels take the
+    full 64 KiB chunks from the device chunk directory (coded-DD for
+    'active', raw-DD for 'ramp'/'rand'), the fused kernel the short last
+    ones; bit-exact vs the oracle, no fallback."""
+    import workloads as W
+    from tiledb_amd.filter_pipeline import Datatype
+    ser = W.c5_pipeline_bytes()
+    op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.INT32), 4)
+    dp = eng.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+    rng = np.random.default_rng(21)
+    vals = [np.concatenate([W.c5_values(variant, 16 * k + c, rng) for c in range(16)])[: 262144 - 9 * k - 1]
+            for k in range(6)]
+    enc = [np.frombuffer(op.filter_tile(v.view(np.uint8)), dtype=np.uint8) for v in vals]
+    assert all(int(np.frombuffer(e[:8].tobytes(), dtype=np.uint64)[0]) == 16 for e in enc)
+    n = 40
+    batch = eng.TileBatch.from_host([enc[i % 6] for i in range(n)], [vals[i % 6].nbytes for i in range(n)])
+    f0, b0, _ = ctx.path_stats()
+    c0 = ctx.stream_chunks()
+    st = ctx.unfilter(dp, batch, chunk_parallel=True)
+    f1, b1, _ = ctx.path_stats()
+    assert not st.any()
+    assert b1 - b0 == 0 and f1 - f0 == n
+    assert ctx.stream_chunks() - c0 == 15 * n  # every full chunk; the short last ones went to the fused kernel
+    out = batch.outputs_host()
+    for i in range(n):
+        o = int(batch.out_off[i])
+        assert np.array_equal(out[o:o + vals[i % 6].nbytes], vals[i % 6].view(np.uint8)), f"tile {i}"

@@ -390,3 +390,27 @@ def test_shuffle4_declined_tiles(eng, ctx, oracle_mod):
     s0 = ctx.stream_tiles()
     _run(eng, ctx, oracle_mod, i16)
     assert ctx.stream_tiles() == s0
+
+
+@pytest.mark.parametrize("cfg", ["c3a", "c3b", "c4"])
+def test_small_chunk_stream_multichunk(eng, ctx, oracle_mod, cfg):
+    """Multi-chunk C3a / C3b / C4 tiles (16 chunks of 8,192 u64 values, the
+    last one short) in a chunk-parallel launch: the small-image streaming
+    kernel takes every full chunk from the device chunk directory, the fused
+    kernel the short last ones; bit-exact vs the oracle."""
+    from tests.test_gpu_parity import check_parity, encode
+    rng = np.random.default_rng(77)
+    gen = W.c4_values if cfg == "c4" else W.c3_values
+    vals = [np.concatenate([gen(16 * k + c, rng) for c in range(16)])[: 131072 - 5 * k - 1] for k in range(4)]
+    ser, dt, cs, _, _ = W.config(cfg)
+    pipe = {"c3a": P(DD()), "c3b": P(RLE()), "c4": _pd_bwr()}[cfg]
+    case = Case(f"{cfg}_multichunk", pipe, dt, cs, [as_u8(v) for v in vals])
+    _, enc = encode(oracle_mod, case)
+    assert len(enc) == 4 and all(int(np.frombuffer(e[0][:8].tobytes(), dtype=np.uint64)[0]) == 16 for e in enc)
+    n = 24
+    f0, b0, _ = ctx.path_stats()
+    c0 = ctx.stream_chunks()
+    check_parity(eng, ctx, oracle_mod, case, [enc[i % 4][0] for i in range(n)], [enc[i % 4][2] for i in range(n)])
+    f1, b1, _ = ctx.path_stats()
+    assert b1 - b0 == 0 and f1 - f0 == n
+    assert ctx.stream_chunks() - c0 == 15 * n

@@ -93,6 +93,14 @@ SIGNATURES = {
     "tdbg_dense_copy_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "tdbg_dense_read_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             ctypes.c_uint64, ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
+    "tdbg_context_stream_chunk_stats": (ctypes.c_int, [c_vp, c_u64p]),
+    "tdbg_dense_copy_fragments_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                       c_vp, c_vp, c_vp]),
+    "tdbg_dense_var_offsets_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                    c_vp, c_vp, c_vp, c_vp]),
+    "tdbg_dense_var_copy_async": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "tdbg_dense_read_var_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_u64p, c_i32p]),
 }
 
 DENSE_MAX_DIMS = 4  # TDBG_DENSE_MAX_DIMS
@@ -112,6 +120,13 @@ class DenseCopyConfig(ctypes.Structure):
                 ("tile_extent", ctypes.c_int64 * DENSE_MAX_DIMS),
                 ("sub_lo", ctypes.c_int64 * DENSE_MAX_DIMS),
                 ("sub_hi", ctypes.c_int64 * DENSE_MAX_DIMS)]
+
+
+class DenseFragConfig(ctypes.Structure):
+    """tdbg_dense_frag_config (several fragments, fill values, var cells)."""
+    _fields_ = [("base", DenseCopyConfig), ("nfrag", ctypes.c_uint32), ("nullable", ctypes.c_uint32),
+                ("fill_size", ctypes.c_uint32), ("fill_validity", ctypes.c_uint32),
+                ("elements_mode", ctypes.c_uint32), ("data_type_size", ctypes.c_uint32)]
 
 for _name, (_res, _args) in SIGNATURES.items():
     _f = getattr(lib, _name)

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "../../include/tiledb_amd.h"
+#include "tdbg_device.h"
 
 namespace tdbg {
 namespace dense {
@@ -135,6 +136,214 @@ __global__ void __launch_bounds__(NT) dense_copy_kernel(const tdbg_dense_copy_co
   }
 }
 
+// ---------------------------------------------------------------------------
+// Several fragments and fill values (DenseReader::copy_fixed_tiles /
+// copy_offset_tiles / fix_offsets_buffer / copy_var_tiles,
+// dense_reader.cc:1199-1236, 1521-2000).  The reference walks a slab's
+// fragment domains from the last to the first, each overwriting the cells it
+// overlaps (cell_slab_overlaps_range :1521-1552: every coordinate inside the
+// domain), and fills what the last one does not write: the surviving value of
+// a cell is the first fragment (lowest fd) whose domain holds it and whose
+// tile exists, else the fill value.  Here one workgroup takes a space tile
+// and its threads take the result cells of the tile's part of the subarray
+// in result order (consecutive threads, consecutive result cells), each
+// finding its fragment and copying one cell.
+// ---------------------------------------------------------------------------
+struct Region {
+  int64_t lo[TDBG_DENSE_MAX_DIMS], len[TDBG_DENSE_MAX_DIMS], toff[TDBG_DENSE_MAX_DIMS];
+  uint64_t ncell;
+};
+
+__device__ __forceinline__ bool region_of(const tdbg_dense_copy_config& cfg, const int64_t* ts, Region& R) {
+  const uint32_t nd = cfg.dim_num;
+  R.ncell = 1;
+  for (uint32_t d = 0; d < nd; d++) {
+    const int64_t a = ts[d] > cfg.sub_lo[d] ? ts[d] : cfg.sub_lo[d];
+    const int64_t e = ts[d] + cfg.tile_extent[d] - 1;
+    const int64_t b = e < cfg.sub_hi[d] ? e : cfg.sub_hi[d];
+    if (b < a) return false;
+    R.lo[d] = a;
+    R.len[d] = b - a + 1;
+    R.toff[d] = a - ts[d];
+    R.ncell *= (uint64_t)R.len[d];
+  }
+  return true;
+}
+
+// cell k of the region in result-layout order: its position in the tile
+// (cell order) and in the result buffer (layout); the fragment that
+// survives there (-1: the fill value)
+__device__ __forceinline__ int cell_at(const tdbg_dense_copy_config& cfg, const Region& R, uint64_t k, uint32_t t,
+                                       uint32_t nfrag, const int64_t* frag_dom, const uint8_t* const* present,
+                                       uint64_t& pos, uint64_t& rc) {
+  const uint32_t nd = cfg.dim_num;
+  const bool trow = cfg.cell_order == 0, rrow = cfg.layout == 0;
+  int64_t c[TDBG_DENSE_MAX_DIMS];
+  uint64_t r = k;
+  if (rrow) {
+    for (int d = (int)nd - 1; d >= 0; d--) {
+      c[d] = (int64_t)(r % (uint64_t)R.len[d]);
+      r /= (uint64_t)R.len[d];
+    }
+  } else {
+    for (uint32_t d = 0; d < nd; d++) {
+      c[d] = (int64_t)(r % (uint64_t)R.len[d]);
+      r /= (uint64_t)R.len[d];
+    }
+  }
+  int64_t ct[TDBG_DENSE_MAX_DIMS], cr[TDBG_DENSE_MAX_DIMS], sub_ext[TDBG_DENSE_MAX_DIMS];
+  for (uint32_t d = 0; d < nd; d++) {
+    ct[d] = R.toff[d] + c[d];
+    cr[d] = R.lo[d] - cfg.sub_lo[d] + c[d];
+    sub_ext[d] = cfg.sub_hi[d] - cfg.sub_lo[d] + 1;
+  }
+  pos = lin(ct, cfg.tile_extent, nd, trow);
+  rc = lin(cr, sub_ext, nd, rrow);
+  for (uint32_t f = 0; f < nfrag; f++) {
+    if (!present[(uint64_t)t * nfrag + f]) continue;
+    const int64_t* dom = frag_dom + (uint64_t)f * nd * 2;
+    bool in = true;
+    for (uint32_t d = 0; d < nd; d++) {
+      const int64_t x = R.lo[d] + c[d];
+      in = in && x >= dom[2 * d] && x <= dom[2 * d + 1];
+    }
+    if (in) return (int)f;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint64_t n) {
+  if (((((uintptr_t)d) | ((uintptr_t)s) | n) & 7) == 0) {
+    for (uint64_t i = 0; i < n / 8; i++) ((uint64_t*)d)[i] = ((const uint64_t*)s)[i];
+  } else if (((((uintptr_t)d) | ((uintptr_t)s) | n) & 3) == 0) {
+    for (uint64_t i = 0; i < n / 4; i++) ((uint32_t*)d)[i] = ((const uint32_t*)s)[i];
+  } else {
+    for (uint64_t i = 0; i < n; i++) d[i] = s[i];
+  }
+}
+
+__global__ void __launch_bounds__(NT) dense_frag_copy_kernel(const tdbg_dense_frag_config fc, uint64_t ntiles,
+                                                             const int64_t* tile_start, const int64_t* frag_dom,
+                                                             const uint8_t* const* tiles,
+                                                             const uint8_t* const* validity,
+                                                             const uint8_t* fill, uint8_t* result,
+                                                             uint8_t* result_validity) {
+  const tdbg_dense_copy_config& cfg = fc.base;
+  const uint64_t cs = cfg.cell_size;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    Region R;
+    if (!region_of(cfg, tile_start + t * cfg.dim_num, R)) continue;
+    for (uint64_t k = threadIdx.x; k < R.ncell; k += NT) {
+      uint64_t pos, rc;
+      const int f = cell_at(cfg, R, k, (uint32_t)t, fc.nfrag, frag_dom, tiles, pos, rc);
+      const uint8_t* src = f >= 0 ? tiles[t * fc.nfrag + f] + pos * cs : fill;
+      copy_bytes(result + rc * cs, src, cs);
+      if (fc.nullable && result_validity)
+        result_validity[rc] = f >= 0 ? validity[t * fc.nfrag + f][pos] : (uint8_t)fc.fill_validity;
+    }
+  }
+}
+
+// copy_offset_tiles + the sentinel half of fix_offsets_buffer: each result
+// cell's size (in elements in elements mode) into offsets[rc] and the address
+// of its bytes into src[rc] (the fill value for cells no fragment writes)
+__global__ void __launch_bounds__(NT) dense_var_sizes_kernel(const tdbg_dense_frag_config fc, uint64_t ntiles,
+                                                             const int64_t* tile_start, const int64_t* frag_dom,
+                                                             const uint8_t* const* off_tiles,
+                                                             const uint8_t* const* var_tiles,
+                                                             const uint8_t* const* validity, const uint8_t* fill,
+                                                             uint64_t* offsets, uint64_t* src,
+                                                             uint8_t* result_validity) {
+  const tdbg_dense_copy_config& cfg = fc.base;
+  const uint64_t div = fc.elements_mode ? fc.data_type_size : 1;
+  const uint64_t fill_units = fc.fill_size / div;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    Region R;
+    if (!region_of(cfg, tile_start + t * cfg.dim_num, R)) continue;
+    for (uint64_t k = threadIdx.x; k < R.ncell; k += NT) {
+      uint64_t pos, rc;
+      const int f = cell_at(cfg, R, k, (uint32_t)t, fc.nfrag, frag_dom, off_tiles, pos, rc);
+      if (f >= 0) {
+        const uint64_t* o = (const uint64_t*)off_tiles[t * fc.nfrag + f];
+        const uint64_t o0 = o[pos], o1 = o[pos + 1];
+        offsets[rc] = (o1 - o0) / div;
+        src[rc] = (uint64_t)(var_tiles[t * fc.nfrag + f] + o0);
+      } else {
+        offsets[rc] = fill_units;
+        src[rc] = (uint64_t)fill;
+      }
+      if (fc.nullable && result_validity)
+        result_validity[rc] = f >= 0 ? validity[t * fc.nfrag + f][pos] : (uint8_t)fc.fill_validity;
+    }
+  }
+}
+
+// exclusive scan of n uint64 in place (fix_offsets_buffer's running
+// var_buffer_size): SB = 2,048 values per block
+constexpr uint32_t SB = NT * 8;
+
+__device__ __forceinline__ uint64_t block_scan_ex(uint64_t v, uint64_t& total, uint64_t* red) {
+  return block_exscan_u64<NT>(v, total, red);
+}
+
+__global__ void __launch_bounds__(NT) scan_sums_kernel(const uint64_t* x, uint64_t n, uint64_t* bsum) {
+  __shared__ uint64_t red[NT / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * SB;
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint64_t j = b0 + (uint64_t)threadIdx.x * 8 + i;
+    s += j < n ? x[j] : 0;
+  }
+  uint64_t tot;
+  (void)block_scan_ex(s, tot, red);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive prefix of the block sums (in place) and the total
+__global__ void __launch_bounds__(NT) scan_prefix_kernel(uint64_t* bsum, uint64_t nb, uint64_t* total) {
+  __shared__ uint64_t red[NT / 64];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < nb; base += NT) {
+    const uint64_t j = base + threadIdx.x;
+    const uint64_t v = j < nb ? bsum[j] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_scan_ex(v, tot, red);
+    if (j < nb) bsum[j] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void __launch_bounds__(NT) scan_apply_kernel(uint64_t* x, uint64_t n, const uint64_t* bsum) {
+  __shared__ uint64_t red[NT / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * SB;
+  uint64_t v[8], s = 0;
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint64_t j = b0 + (uint64_t)threadIdx.x * 8 + i;
+    v[i] = j < n ? x[j] : 0;
+    s += v[i];
+  }
+  uint64_t tot;
+  uint64_t run = bsum[blockIdx.x] + block_scan_ex(s, tot, red);
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint64_t j = b0 + (uint64_t)threadIdx.x * 8 + i;
+    if (j < n) x[j] = run;
+    run += v[i];
+  }
+}
+
+// copy_var_tiles: every result cell's bytes to its offset (times the type
+// size in elements mode); the last cell ends at the total
+__global__ void __launch_bounds__(NT) dense_var_copy_kernel(const uint64_t* offsets, const uint64_t* src, uint64_t n,
+                                                            const uint64_t* total, uint64_t mult, uint8_t* var_out) {
+  const uint64_t tot = *total;
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
+    const uint64_t o = offsets[i];
+    const uint64_t e = i + 1 < n ? offsets[i + 1] : tot;
+    copy_bytes(var_out + o * mult, (const uint8_t*)src[i], (e - o) * mult);
+  }
+}
+
 }  // namespace dense
 }  // namespace tdbg
 
@@ -145,5 +354,44 @@ extern "C" hipError_t tdbg_launch_dense_copy(const tdbg_dense_copy_config* cfg, 
   if (ntiles == 0) return hipSuccess;
   hipLaunchKernelGGL(tdbg::dense::dense_copy_kernel, dim3(grid), dim3(tdbg::dense::NT), 0, s, *cfg, ntiles,
                      tile_start, tiles, status, result);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tdbg_launch_dense_frag_copy(const tdbg_dense_frag_config* fc, uint64_t ntiles,
+                                                  const int64_t* tile_start, const int64_t* frag_dom,
+                                                  const uint8_t* const* tiles, const uint8_t* const* validity,
+                                                  const uint8_t* fill, uint8_t* result, uint8_t* result_validity,
+                                                  uint32_t grid, hipStream_t s) {
+  if (ntiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(tdbg::dense::dense_frag_copy_kernel, dim3(grid), dim3(tdbg::dense::NT), 0, s, *fc, ntiles,
+                     tile_start, frag_dom, tiles, validity, fill, result, result_validity);
+  return hipGetLastError();
+}
+
+// sizes -> exclusive offsets in place (+ total); bsum: (n + 2047) / 2048 entries
+extern "C" hipError_t tdbg_launch_dense_var_offsets(const tdbg_dense_frag_config* fc, uint64_t ntiles,
+                                                    const int64_t* tile_start, const int64_t* frag_dom,
+                                                    const uint8_t* const* off_tiles, const uint8_t* const* var_tiles,
+                                                    const uint8_t* const* validity, const uint8_t* fill,
+                                                    uint64_t* offsets, uint64_t ncells, uint64_t* src,
+                                                    uint8_t* result_validity, uint64_t* bsum, uint64_t* total,
+                                                    uint32_t grid, hipStream_t s) {
+  using namespace tdbg::dense;
+  if (ntiles)
+    hipLaunchKernelGGL(dense_var_sizes_kernel, dim3(grid), dim3(NT), 0, s, *fc, ntiles, tile_start, frag_dom,
+                       off_tiles, var_tiles, validity, fill, offsets, src, result_validity);
+  const uint64_t nb = (ncells + SB - 1) / SB;
+  if (nb) hipLaunchKernelGGL(scan_sums_kernel, dim3((uint32_t)nb), dim3(NT), 0, s, offsets, ncells, bsum);
+  hipLaunchKernelGGL(scan_prefix_kernel, dim3(1), dim3(NT), 0, s, bsum, nb, total);
+  if (nb) hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(NT), 0, s, offsets, ncells, bsum);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tdbg_launch_dense_var_copy(const uint64_t* offsets, const uint64_t* src, uint64_t ncells,
+                                                 const uint64_t* total, uint64_t mult, uint8_t* var_out,
+                                                 uint32_t grid, hipStream_t s) {
+  if (ncells == 0) return hipSuccess;
+  hipLaunchKernelGGL(tdbg::dense::dense_var_copy_kernel, dim3(grid), dim3(tdbg::dense::NT), 0, s, offsets, src,
+                     ncells, total, mult, var_out);
   return hipGetLastError();
 }

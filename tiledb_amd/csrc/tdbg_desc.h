@@ -59,7 +59,8 @@ enum tdbg_stat_slot : uint32_t {
   TDBG_STAT_STREAM_TILES = 5,   // of the fused tiles: those the streaming C5 kernels took (tdbg_stream*.hip)
   TDBG_STAT_STREAM_RAW_TILES = 6,  // of those: the raw-DoubleDelta kernel's (tdbg_stream_raw.hip)
   TDBG_STAT_FWD_STREAM_TILES = 7,  // forward: tiles the LDS-resident C5 kernel filtered (tdbg_forward_stream.hip)
-  TDBG_STAT_N = 8
+  TDBG_STAT_STREAM_CHUNKS = 8,  // chunk-parallel launches: chunks the streaming kernels took
+  TDBG_STAT_N = 9
 };
 
 // host-side internals shared by tdbg_host.cpp and tdbg_cpu.cpp

@@ -2198,9 +2198,17 @@ unfilter_fused_kernel(const KParams kp) {
     // fused path declines sends its whole tile to the general interpreter
     // (first decline wins the status, queues the tile, and takes it out of
     // the fused counters the directory pass added it to)
-    const uint32_t nck = __builtin_amdgcn_readfirstlane(*kp.nchunks);
+    // (after the streaming kernels' chunk-mode launch: only the chunks they
+    // queued, kp.tile_list[0 .. *kp.ntiles_dev))
+    uint32_t nck = __builtin_amdgcn_readfirstlane(*kp.nchunks);
+    const uint32_t* cl = nullptr;
+    if (kp.ntiles_dev) {
+      const uint32_t q = __builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
+      nck = q < kp.ntiles ? q : (uint32_t)kp.ntiles;
+      cl = kp.tile_list;
+    }
     for (uint32_t j = blockIdx.x; j < nck; j += (uint32_t)G) {
-      const ChunkRec* rp = kp.chunks + j;
+      const ChunkRec* rp = kp.chunks + (cl ? __builtin_amdgcn_readfirstlane(cl[j]) : j);
       const uint32_t tile = __builtin_amdgcn_readfirstlane(rp->tile);
       const uint32_t ml = __builtin_amdgcn_readfirstlane(rp->ml);
       const uint32_t fl = __builtin_amdgcn_readfirstlane(rp->fl);

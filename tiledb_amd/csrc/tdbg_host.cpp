@@ -59,6 +59,21 @@ extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t
                                                hipStream_t s);
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
 extern "C" hipError_t tdbg_launch_stream_shuffle4(const tdbg::KParams* kp, hipStream_t s);
+extern "C" hipError_t tdbg_launch_dense_frag_copy(const tdbg_dense_frag_config* fc, uint64_t ntiles,
+                                                  const int64_t* tile_start, const int64_t* frag_dom,
+                                                  const uint8_t* const* tiles, const uint8_t* const* validity,
+                                                  const uint8_t* fill, uint8_t* result, uint8_t* result_validity,
+                                                  uint32_t grid, hipStream_t s);
+extern "C" hipError_t tdbg_launch_dense_var_offsets(const tdbg_dense_frag_config* fc, uint64_t ntiles,
+                                                    const int64_t* tile_start, const int64_t* frag_dom,
+                                                    const uint8_t* const* off_tiles, const uint8_t* const* var_tiles,
+                                                    const uint8_t* const* validity, const uint8_t* fill,
+                                                    uint64_t* offsets, uint64_t ncells, uint64_t* src,
+                                                    uint8_t* result_validity, uint64_t* bsum, uint64_t* total,
+                                                    uint32_t grid, hipStream_t s);
+extern "C" hipError_t tdbg_launch_dense_var_copy(const uint64_t* offsets, const uint64_t* src, uint64_t ncells,
+                                                 const uint64_t* total, uint64_t mult, uint8_t* var_out,
+                                                 uint32_t grid, hipStream_t s);
 extern "C" hipError_t tdbg_launch_dense_copy(const tdbg_dense_copy_config* cfg, uint64_t ntiles,
                                              const int64_t* tile_start, const uint8_t* const* tiles,
                                              const int32_t* status, uint8_t* result, uint32_t grid,
@@ -159,6 +174,11 @@ struct tdbg_context {
   // directory pass): later launches size the directory from it
   volatile uint64_t* dir_need = nullptr;
   uint64_t* dir_need_dev = nullptr;
+  // dense var reads: each result cell's source address (step 1 -> step 2)
+  // and the scan's block sums
+  uint64_t* dense_src = nullptr;
+  uint64_t dense_src_cap = 0, dense_ncells = 0;
+  uint64_t* dense_bsum = nullptr;
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -172,6 +192,10 @@ struct tdbg_context {
   // streaming C5 kernel's queue (KParams::sq): the tiles it leaves to the
   // fused kernel, count + status_cap entries
   uint32_t* d_sq = nullptr;
+  // chunk-mode streaming launches: the chunks the streaming kernels leave to
+  // the fused kernel (count + cq_cap entries), cleared before every launch
+  uint32_t* d_cq = nullptr;
+  uint64_t cq_cap = 0;
   // d_sq[0] is 0 (the last streamed launch's fixup kernel reset it), so the
   // next streamed launch needs no memset for it
   bool sq_clean = true;
@@ -551,6 +575,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->d_list) (void)hipFree(c->d_list);
   if (c->d_fbq) (void)hipFree(c->d_fbq);
   if (c->d_sq) (void)hipFree(c->d_sq);
+  if (c->d_cq) (void)hipFree(c->d_cq);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->rscratch) (void)hipFree(c->rscratch);
   if (c->fscratch) (void)hipFree(c->fscratch);
@@ -559,6 +584,8 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->dir_recs) (void)hipFree(c->dir_recs);
   if (c->dir_total) (void)hipFree(c->dir_total);
   if (c->dir_need) (void)hipHostFree((void*)c->dir_need);
+  if (c->dense_src) (void)hipFree(c->dense_src);
+  if (c->dense_bsum) (void)hipFree(c->dense_bsum);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -714,7 +741,24 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("chunk directory launch: ") + hipGetErrorString(e));
     kp.chunks = c->dir_recs;
     kp.nchunks = c->dir_total;
+    if ((c5_stream || small_mode >= 0) && !no_stream && !d_list) {
+      // the streaming kernels take the directory's chunk records; their
+      // queue holds chunk indices
+      if (c->cq_cap < c->dir_cap) {
+        HIP_OK(hipStreamSynchronize(stream));  // an earlier launch may still read the old queue
+        if (c->d_cq) HIP_OK(hipFree(c->d_cq));
+        c->d_cq = nullptr;
+        c->cq_cap = 0;
+        HIP_OK(hipMalloc(&c->d_cq, (c->dir_cap + 1) * sizeof(uint32_t)));
+        c->cq_cap = c->dir_cap;
+      }
+      HIP_OK(hipMemsetAsync(c->d_cq, 0, sizeof(uint32_t), stream));
+    }
   }
+  // the headline pipeline's streaming kernels on chunk records (chunk-parallel
+  // launches of multi-chunk tiles, SURVEY 8(a) FilterPipeline::run_reverse's
+  // loop over chunks, filter_pipeline.cc:439-517)
+  const bool chunk_stream = chunked && (c5_stream || small_mode >= 0) && !no_stream && !d_list && c->d_cq != nullptr;
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
   // Events only on armed launches (tdbg_context_time_launches): an event
   // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
@@ -722,7 +766,33 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   hipError_t e = hipSuccess;
   static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
   static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
-  if (streamed) {
+  if (chunk_stream) {
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(c->cq_cap, 0xffffffffull);
+    tdbg::KParams ks = kp;
+    ks.ntiles = cap;
+    ks.ntiles_dev = c->dir_total;
+    ks.sq = c->d_cq;
+    ks.sq_cap = cap;
+    ks.fbq = nullptr;  // (cleared before the directory pass, which may append)
+    if (small_mode >= 0) {
+      const int sgn = (small_mode == 2 && P.s[1].sgn) ? 1 : 0;
+      if (!skip_fused)
+        e = tdbg_launch_stream_small(&ks, tdbg_stream_small_grid(c->cus, small_mode), small_mode, sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
+    } else {
+      const int sgn = p->plan.s[2].sgn ? 1 : 0;
+      if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+      if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
+    }
+    tdbg::KParams kf = kp;  // the fused kernel on the chunks they queued
+    kf.ntiles = cap;
+    kf.tile_list = c->d_cq + 1;
+    kf.ntiles_dev = c->d_cq;
+    if (!skip_fused) e = tdbg_launch_fast(&kf, grid, stream);
+    if (te) HIP_OK(hipEventRecord(te[1], stream));
+  } else if (streamed) {
     tdbg::KParams ks = kp;
     ks.sq = c->d_sq;
     ks.sq_cap = (uint32_t)ntiles;
@@ -1156,6 +1226,15 @@ int tdbg_context_stream_stats(const tdbg_context* c, uint64_t* stream_tiles) {
   int rc = read_stats(c, h);
   if (rc) return rc;
   if (stream_tiles) *stream_tiles = h[TDBG_STAT_STREAM_TILES];
+  return TDBG_OK;
+}
+
+int tdbg_context_stream_chunk_stats(const tdbg_context* c, uint64_t* chunks) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (chunks) *chunks = h[TDBG_STAT_STREAM_CHUNKS];
   return TDBG_OK;
 }
 
@@ -1814,6 +1893,257 @@ int tdbg_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
 int tdbg_device_count(int* n) {
   if (!n) return fail(TDBG_E_ARG, "null out");
   HIP_OK(hipGetDeviceCount(n));
+  return TDBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// dense reads with several fragments / fill values / var-sized cells
+// (dense_reader.cc:1199-1236, 1521-2000; tdbg_dense.hip)
+// ---------------------------------------------------------------------------
+static bool frag_cfg_ok(const tdbg_dense_frag_config* f, bool var) {
+  if (!f || !dense_cfg_ok(&f->base)) return false;
+  if (f->fill_validity > 1) return false;
+  if (var) {
+    if (f->elements_mode && (f->data_type_size == 0 || f->fill_size % f->data_type_size)) return false;
+  } else if (f->fill_size != f->base.cell_size) {
+    return false;
+  }
+  return true;
+}
+
+static uint64_t dense_cells(const tdbg_dense_copy_config* g) {
+  uint64_t n = 1;
+  for (uint32_t d = 0; d < g->dim_num; d++) n *= (uint64_t)(g->sub_hi[d] - g->sub_lo[d] + 1);
+  return n;
+}
+
+int tdbg_dense_copy_fragments_async(tdbg_context* c, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
+                                    const int64_t* d_tile_start, const int64_t* d_frag_dom,
+                                    const uint8_t* const* d_tiles, const uint8_t* const* d_validity,
+                                    const uint8_t* d_fill_value, uint8_t* d_result, uint8_t* d_result_validity,
+                                    tdbg_stream stream) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (!frag_cfg_ok(cfg, false)) return fail(TDBG_E_ARG, "invalid dense fragment copy config");
+  if (ntiles == 0) return TDBG_OK;
+  if (!d_tile_start || !d_result || !d_fill_value || (cfg->nfrag && (!d_tiles || !d_frag_dom)))
+    return fail(TDBG_E_ARG, "null dense copy arrays");
+  if (cfg->nullable && (!d_result_validity || (cfg->nfrag && !d_validity)))
+    return fail(TDBG_E_ARG, "nullable copy without validity buffers");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
+  hipError_t e = tdbg_launch_dense_frag_copy(cfg, ntiles, d_tile_start, d_frag_dom, d_tiles, d_validity, d_fill_value,
+                                             d_result, d_result_validity, grid, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense copy launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+int tdbg_dense_var_offsets_async(tdbg_context* c, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
+                                 const int64_t* d_tile_start, const int64_t* d_frag_dom,
+                                 const uint8_t* const* d_offset_tiles, const uint8_t* const* d_var_tiles,
+                                 const uint8_t* const* d_validity, const uint8_t* d_fill_value,
+                                 uint64_t* d_result_offsets, uint8_t* d_result_validity, uint64_t* d_var_total,
+                                 tdbg_stream stream) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (!frag_cfg_ok(cfg, true)) return fail(TDBG_E_ARG, "invalid dense var copy config");
+  if (!d_result_offsets || !d_var_total || !d_fill_value || (ntiles && !d_tile_start) ||
+      (ntiles && cfg->nfrag && (!d_offset_tiles || !d_var_tiles || !d_frag_dom)))
+    return fail(TDBG_E_ARG, "null dense var arrays");
+  if (cfg->nullable && (!d_result_validity || (cfg->nfrag && !d_validity)))
+    return fail(TDBG_E_ARG, "nullable copy without validity buffers");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  const uint64_t n = dense_cells(&cfg->base);
+  const uint64_t nb = (n + 2047) / 2048;
+  if (n > c->dense_src_cap) {
+    HIP_OK(hipStreamSynchronize((hipStream_t)stream));  // an earlier step 2 may still read them
+    if (c->dense_src) HIP_OK(hipFree(c->dense_src));
+    if (c->dense_bsum) HIP_OK(hipFree(c->dense_bsum));
+    c->dense_src = nullptr;
+    c->dense_bsum = nullptr;
+    c->dense_src_cap = 0;
+    HIP_OK(hipMalloc(&c->dense_src, n * 8));
+    HIP_OK(hipMalloc(&c->dense_bsum, std::max<uint64_t>(nb, 1) * 8));
+    c->dense_src_cap = n;
+  }
+  c->dense_ncells = n;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), (uint64_t)c->cus * 8);
+  hipError_t e = tdbg_launch_dense_var_offsets(cfg, ntiles, d_tile_start, d_frag_dom, d_offset_tiles, d_var_tiles,
+                                               d_validity, d_fill_value, d_result_offsets, n, c->dense_src,
+                                               d_result_validity, c->dense_bsum, d_var_total, grid,
+                                               (hipStream_t)stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense var offsets launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+int tdbg_dense_var_copy_async(tdbg_context* c, const tdbg_dense_frag_config* cfg, const uint64_t* d_result_offsets,
+                              const uint64_t* d_var_total, uint8_t* d_result_var, tdbg_stream stream) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  if (!frag_cfg_ok(cfg, true)) return fail(TDBG_E_ARG, "invalid dense var copy config");
+  if (!d_result_offsets || !d_var_total || !d_result_var) return fail(TDBG_E_ARG, "null dense var arrays");
+  const uint64_t n = dense_cells(&cfg->base);
+  if (n != c->dense_ncells || !c->dense_src)
+    return fail(TDBG_E_ARG, "tdbg_dense_var_copy_async: run tdbg_dense_var_offsets_async on this context first");
+  HIP_OK(hipSetDevice(c->device));
+  int rc = order_stream(c, (hipStream_t)stream);
+  if (rc) return rc;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)c->cus * 8);
+  hipError_t e = tdbg_launch_dense_var_copy(d_result_offsets, c->dense_src, n, d_var_total,
+                                            cfg->elements_mode ? cfg->data_type_size : 1, d_result_var, grid,
+                                            (hipStream_t)stream);
+  if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense var copy launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdbg_pipeline* pv,
+                             const tdbg_dense_frag_config* cfg, uint64_t ntiles, const int64_t* tile_start,
+                             const int64_t* frag_dom, const uint8_t* const* off_filtered,
+                             const uint64_t* off_filtered_size, const uint8_t* const* var_filtered,
+                             const uint64_t* var_filtered_size, const uint64_t* var_unfiltered_size,
+                             const uint8_t* fill_value, uint64_t* result_offsets, uint8_t* result_var,
+                             uint64_t var_cap, uint64_t* var_total, int32_t* host_status) {
+  if (!c || !po || !pv) return fail(TDBG_E_ARG, "null context or pipeline");
+  if (!po->supported || !pv->supported) return fail(TDBG_E_UNSUPPORTED, "pipeline has a filter the engine does not run");
+  if (!frag_cfg_ok(cfg, true) || cfg->nullable) return fail(TDBG_E_ARG, "invalid dense var read config");
+  if (!result_offsets || !var_total || (cfg->fill_size && !fill_value))
+    return fail(TDBG_E_ARG, "null dense var read outputs");
+  const uint32_t nd = cfg->base.dim_num, nf = cfg->nfrag;
+  const uint64_t npair = ntiles * nf;
+  if (npair && (!tile_start || !frag_dom || !off_filtered || !off_filtered_size || !var_filtered ||
+                !var_filtered_size || !var_unfiltered_size))
+    return fail(TDBG_E_ARG, "null dense var read inputs");
+  HIP_OK(hipSetDevice(c->device));
+  if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  hipStream_t s = c->cstream;
+  int rc = order_stream(c, s);
+  if (rc) return rc;
+  uint64_t cells_per_tile = 1;
+  for (uint32_t d = 0; d < nd; d++) cells_per_tile *= (uint64_t)cfg->base.tile_extent[d];
+  // the present (tile, fragment) pairs: filtered bytes in, unfiltered out
+  std::vector<uint64_t> idx;
+  uint64_t fin = 0, unf_off = 0, unf_var = 0;
+  for (uint64_t i = 0; i < npair; i++)
+    if (off_filtered[i]) {
+      if (!var_filtered[i]) return fail(TDBG_E_ARG, "offsets tile without its var tile");
+      idx.push_back(i);
+      fin += off_filtered_size[i] + var_filtered_size[i];
+      unf_off += (cells_per_tile + 1) * 8;
+      unf_var += var_unfiltered_size[i];
+    }
+  const uint64_t m = idx.size();
+  const uint64_t n = dense_cells(&cfg->base);
+  std::vector<void*> bufs;
+  auto dalloc = [&](void** out, uint64_t bytes) -> bool {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<uint64_t>(bytes, 16)) != hipSuccess) return false;
+    bufs.push_back(q);
+    *out = q;
+    return true;
+  };
+  struct Free {
+    std::vector<void*>& b;
+    ~Free() {
+      for (void* q : b) (void)hipFree(q);
+    }
+  } free_all{bufs};
+  uint8_t *d_in = nullptr, *d_off = nullptr, *d_var = nullptr, *d_fill = nullptr;
+  int64_t *d_start = nullptr, *d_dom = nullptr;
+  uint64_t* d_ptr = nullptr;  // unfilter tables for the 2m tiles, then per-pair tile tables
+  int32_t* d_st = nullptr;
+  uint64_t *d_roff = nullptr, *d_total = nullptr;
+  if (!dalloc((void**)&d_in, fin) || !dalloc((void**)&d_off, unf_off) || !dalloc((void**)&d_var, unf_var) ||
+      !dalloc((void**)&d_fill, cfg->fill_size) || !dalloc((void**)&d_start, ntiles * nd * 8) ||
+      !dalloc((void**)&d_dom, (uint64_t)nf * nd * 16) || !dalloc((void**)&d_ptr, (9 * m + 2 * npair) * 8) ||
+      !dalloc((void**)&d_st, 2 * m * 4) || !dalloc((void**)&d_roff, n * 8) || !dalloc((void**)&d_total, 8))
+    return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+  // [2m in][2m in size][2m out][2m out size][m var size][npair offsets tile][npair var tile]
+  std::vector<uint64_t> h(9 * m + 2 * npair, 0);
+  uint64_t* hin = h.data();
+  uint64_t* hisz = hin + 2 * m;
+  uint64_t* hout = hisz + 2 * m;
+  uint64_t* hosz = hout + 2 * m;
+  uint64_t* hvsz = hosz + 2 * m;
+  uint64_t* hoff_t = hvsz + m;
+  uint64_t* hvar_t = hoff_t + npair;
+  uint64_t io = 0, oo = 0, ov = 0;
+  for (uint64_t k = 0; k < m; k++) {
+    const uint64_t i = idx[k];
+    HIP_OK(hipMemcpyAsync(d_in + io, off_filtered[i], off_filtered_size[i], hipMemcpyHostToDevice, s));
+    hin[k] = (uint64_t)(uintptr_t)(d_in + io);
+    hisz[k] = off_filtered_size[i];
+    io += off_filtered_size[i];
+    HIP_OK(hipMemcpyAsync(d_in + io, var_filtered[i], var_filtered_size[i], hipMemcpyHostToDevice, s));
+    hin[m + k] = (uint64_t)(uintptr_t)(d_in + io);
+    hisz[m + k] = var_filtered_size[i];
+    io += var_filtered_size[i];
+    hout[k] = (uint64_t)(uintptr_t)(d_off + oo);
+    hosz[k] = (cells_per_tile + 1) * 8;
+    hoff_t[i] = hout[k];
+    oo += hosz[k];
+    hout[m + k] = (uint64_t)(uintptr_t)(d_var + ov);
+    hosz[m + k] = var_unfiltered_size[i];
+    hvar_t[i] = hout[m + k];
+    ov += var_unfiltered_size[i];
+    hvsz[k] = var_unfiltered_size[i];
+  }
+  HIP_OK(hipMemcpyAsync(d_ptr, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+  if (cfg->fill_size) HIP_OK(hipMemcpyAsync(d_fill, fill_value, cfg->fill_size, hipMemcpyHostToDevice, s));
+  if (ntiles) HIP_OK(hipMemcpyAsync(d_start, tile_start, ntiles * nd * 8, hipMemcpyHostToDevice, s));
+  if (nf) HIP_OK(hipMemcpyAsync(d_dom, frag_dom, (uint64_t)nf * nd * 16, hipMemcpyHostToDevice, s));
+  const uint64_t* dp = d_ptr;
+  std::vector<int32_t> st(2 * m, 0);
+  if (m) {
+    rc = ensure_status(c, 2 * m);
+    if (rc) return rc;
+    // offsets tiles (the extra slot left for add_extra_offset), then
+    // Tile::add_extra_offset with the var tile's size (reader_base.cc:885-893),
+    // then the var tiles
+    rc = launch(c, po, m, (const uint8_t* const*)dp, dp + 2 * m, (uint8_t* const*)(dp + 4 * m), dp + 6 * m,
+                TDBG_TILE_OFFSETS, d_st, c->d_need, nullptr, s, false);
+    if (rc) return rc;
+    hipError_t e = tdbg_launch_extra_offset(m, (uint8_t* const*)(dp + 4 * m), dp + 6 * m, dp + 8 * m, d_st, s);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("extra offset launch: ") + hipGetErrorString(e));
+    rc = launch(c, pv, m, (const uint8_t* const*)(dp + m), dp + 3 * m, (uint8_t* const*)(dp + 5 * m), dp + 7 * m, 0,
+                d_st + m, c->d_need, nullptr, s, false);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(st.data(), d_st, 2 * m * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  // per pair: the first failure of its two tiles; any failure stops the read
+  // (an unfilter error fails the reference's query)
+  std::vector<int32_t> pst(npair, 0);
+  int first_err = TDBG_OK;
+  for (uint64_t k = 0; k < m; k++) {
+    const int32_t a = st[k] ? st[k] : st[m + k];
+    pst[idx[k]] = a;
+    if (a && first_err == TDBG_OK) first_err = a;
+  }
+  if (host_status && npair) memcpy(host_status, pst.data(), npair * 4);
+  if (first_err != TDBG_OK) return fail(first_err, "dense var read: a tile failed to unfilter");
+  tdbg_dense_frag_config g = *cfg;
+  g.base.cell_size = 8;
+  rc = tdbg_dense_var_offsets_async(c, &g, ntiles, d_start, d_dom, (const uint8_t* const*)(dp + 9 * m),
+                                    (const uint8_t* const*)(dp + 9 * m + npair), nullptr, d_fill, d_roff, nullptr,
+                                    d_total, s);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(var_total, d_total, 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(result_offsets, d_roff, n * 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  const uint64_t mult = cfg->elements_mode ? cfg->data_type_size : 1;
+  const uint64_t vbytes = *var_total * mult;
+  if (vbytes > var_cap || (vbytes && !result_var))
+    return fail(TDBG_E_OUT_FULL, "dense var read: var buffer too small");
+  if (vbytes) {
+    uint8_t* d_rvar = nullptr;
+    if (!dalloc((void**)&d_rvar, vbytes)) return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+    rc = tdbg_dense_var_copy_async(c, &g, d_roff, d_total, d_rvar, s);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(result_var, d_rvar, vbytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  c->tiles_unfiltered += 2 * m;
   return TDBG_OK;
 }
 

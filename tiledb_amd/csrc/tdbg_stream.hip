@@ -176,6 +176,24 @@ __device__ __forceinline__ v4u bwr_unit8(const Lds& L, const Win& W, uint32_t u,
              bfe8<SGN>(r0, 24, 8) + mn};
 }
 
+// 8-bit or raw windows (the wave checked that no lane meets a 16-bit window
+// or a unit past the stream): the four dwords of a raw window's unit, or the
+// four bytes of an 8-bit window's unit widened, chosen per lane
+template <bool SGN>
+__device__ __forceinline__ v4u bwr_unit8r(const Lds& L, const Win& W, uint32_t u, uint32_t w, uint2 te) {
+  const bool raw = (te.x >> 16) != 0;
+  const uint32_t a = (te.x & 0xffffu) + ((u - (w << W.wsh)) << (raw ? 4 : 2));
+  const uint32_t* p = L.C + (a >> 2);
+  const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+  const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, W.sh);
+  const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, W.sh);
+  const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, W.sh);
+  const uint32_t r3 = __builtin_amdgcn_alignbyte(d4, d3, W.sh);
+  const uint32_t mn = te.y;
+  return v4u{raw ? r0 : bfe8<SGN>(r0, 0, 8) + mn, raw ? r1 : bfe8<SGN>(r0, 8, 8) + mn,
+             raw ? r2 : bfe8<SGN>(r0, 16, 8) + mn, raw ? r3 : bfe8<SGN>(r0, 24, 8) + mn};
+}
+
 // ---------------------------------------------------------------------------
 // DD⁻¹ codes of one lane and plane (code width CB = bitsize + 1)
 // ---------------------------------------------------------------------------
@@ -186,12 +204,9 @@ __device__ __forceinline__ v4u bwr_unit8(const Lds& L, const Win& W, uint32_t u,
 // alignbyte(G[x+1], G[x], 2) are the dwords at byte offset 2, and the
 // MSB-first dword sequence swaps the halves of every word.
 template <int CB>
-__device__ __forceinline__ void dd_codes(const uint32_t (&G)[20], uint32_t p, uint32_t n, bool first,
+__device__ __forceinline__ void dd_codes(const uint32_t (&H)[18], uint32_t p, uint32_t n, bool first,
                                          uint32_t x0, uint32_t x1, uint32_t (&xl)[16], uint32_t& Aout,
                                          uint32_t& Bout) {
-  uint32_t H[18];
-#pragma unroll
-  for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
   // M_j = p ? H[(j+1)^1] : H[j^1] as a bit select (v_bfi_b32): a plain
   // ternary lets the optimizer turn the pair into an indexed scratch load
   uint32_t pm = 0u - p;
@@ -230,10 +245,24 @@ __device__ __forceinline__ void dd_codes(const uint32_t (&G)[20], uint32_t p, ui
   Bout = xrun;
 }
 
+#ifndef TDBG_H_MISALIGNED
+#define TDBG_H_MISALIGNED 1
+#endif
+typedef uint32_t u32_a2 __attribute__((aligned(2)));
+
 template <int CB>
 __device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uint32_t p, uint32_t n,
                                             bool first, uint32_t x0, uint32_t x1, uint32_t (&xl)[16],
                                             uint32_t& A, uint32_t& B) {
+  uint32_t H[18];
+#if TDBG_H_MISALIGNED
+  // H[x] = the dword at byte 2 of scratch dword g + x: one 2-byte-aligned
+  // ds_read_b32 each (gfx950 LDS reads any alignment) instead of aligned
+  // pairs and a v_alignbyte
+  const uint8_t* b8 = (const uint8_t*)(wsp + g) + 2;
+#pragma unroll
+  for (int x = 0; x < 18; x++) H[x] = *(const u32_a2*)(b8 + 4 * x);
+#else
   uint32_t G[20];
 #pragma unroll
   for (int x = 0; x < 10; x++) {
@@ -241,7 +270,10 @@ __device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uin
     G[2 * x] = v.x;
     G[2 * x + 1] = v.y;
   }
-  dd_codes<CB>(G, p, n, first, x0, x1, xl, A, B);
+#pragma unroll
+  for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
+#endif
+  dd_codes<CB>(H, p, n, first, x0, x1, xl, A, B);
 }
 
 // ---------------------------------------------------------------------------
@@ -315,19 +347,25 @@ __device__ __forceinline__ void plane(Lds& L, const Win& W, uint32_t w, uint32_t
   // the reads
   uint32_t uu[4], wc[4];
   uint2 te[4];
-  bool gen = false;
+  bool gen = false, k16 = false;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     uu[r] = ulo + 64 * r + l;
     const uint32_t wu = uu[r] >> W.wsh;
     wc[r] = wu < W.wlast ? wu : W.wlast;
     te[r] = L.TAB[wc[r]];
-    gen |= (te[r].x >> 16) != 0 || wu > W.wlast;
+    const uint32_t kind = te[r].x >> 16;
+    gen |= kind != 0 || wu > W.wlast;
+    k16 |= kind == 1 || wu > W.wlast;
   }
   v4u dv[4];
   if (__builtin_amdgcn_ballot_w64(gen) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; r++) dv[r] = bwr_unit8<SGN>(L, W, uu[r], wc[r], te[r]);
+  } else if (__builtin_amdgcn_ballot_w64(k16) == 0) {
+    // 8-bit and raw windows (C5 'active': most wave-planes meet a raw one)
+#pragma unroll
+    for (int r = 0; r < 4; r++) dv[r] = bwr_unit8r<SGN>(L, W, uu[r], wc[r], te[r]);
   } else {
     // (rare: one unit at a time, so the general decoder's temporaries do
     // not set the kernel's register count)
@@ -437,7 +475,7 @@ __device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, ui
     // sq_cap = ntiles -- but a tile that would not fit must not be lost: it
     // gets a status instead of silently keeping whatever its status held)
     if (k < kp.sq_cap) kp.sq[1 + k] = t;
-    else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
+    else if (kp.status) kp.status[kp.chunks ? kp.chunks[t].tile : t] = TDBG_E_INTERNAL;
   }
 }
 
@@ -451,8 +489,10 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     ntl = c < ntl ? c : ntl;
   }
   // the fused kernel's fallback queue starts empty for this launch (it runs
-  // next on the same stream and is the only one to append)
+  // next on the same stream and is the only one to append; chunk mode: the
+  // host cleared it before the directory pass, which may append)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
+  const bool chunked = kp.chunks != nullptr;
   const uint32_t w = wave_();
   Clock pc;
   pc.init(kp.prof, L.clk);
@@ -496,13 +536,16 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     // checks then decide.  BWR md: [u32 orig][u32 nwin] + nwin x [i32 min]
     // [u8 bits][u32 nbytes] (bit_width_reduction_filter.cc:353-380), then the
     // compression frame's md (compression_filter.cc:413-486).
+    // the chunk header sits after the tile's u64 chunk count, or (chunk mode)
+    // the image starts with it
+    const uint32_t ho = chunked ? 0u : 8u;
     const uint32_t b = (uint32_t)((uintptr_t)cur.in & 15);
-    const uint32_t m = b + 20;
+    const uint32_t m = b + ho + 12;
     uint32_t ml = 0, fl = 0, dst = 0, nwin = 0, wsh = 0, ws = 0;
     if (ok) {
-      const uint32_t nlo = c32(L, b), nhi = c32(L, b + 4), orig = c32(L, b + 8);
-      fl = c32(L, b + 12);
-      ml = c32(L, b + 16);
+      const uint32_t nlo = c32(L, b), nhi = c32(L, b + 4), orig = c32(L, b + ho);
+      fl = c32(L, b + ho + 4);
+      ml = c32(L, b + ho + 8);
       const uint32_t Lb = c32(L, m), nwr = c32(L, m + 4), ws0 = c32(L, m + 13);
       // Wave w parses windows [64 w, 64 w + 64), lane l window 64 w + l (9
       // bytes at e0), and writes their table entries with offsets relative
@@ -522,7 +565,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
                      d4 = c32(L, f + 16), d5 = c32(L, f + 20);
       dst = m + ml;
       ws = nwin > 1 ? ws0 : 256;
-      ok = nlo == 1 && nhi == 0 && orig == NV * 4 && (uint64_t)ml + fl + 20 <= cur.fs && nwr >= 1 &&
+      ok = (chunked || (nlo == 1 && nhi == 0)) && orig == NV * 4 && (uint64_t)ml + fl + ho + 12 <= cur.fs && nwr >= 1 &&
            nwr <= TABN && ml == 8 + 9 * nwr + 24 && d0 == 1 && d1 == 1 && d2 == 8 && d3 == 17 &&
            d4 == NV * 4 && d5 + 17 == Lb && ws >= 64 && ws <= 4096 && (ws & (ws - 1)) == 0 &&
            (Lb - 1) / ws + 1 == nwin;
@@ -641,23 +684,31 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       // instruction writes 8 whole 128-B lines (8 lanes per line).
       uint8_t* o = cur.out + 16u * (1024u * w);
       uint32_t* wsp = L.WS[w];
+      // the 4x4 byte transposes of all 16 units, every lane active, in place
+      // (unit i's four output dwords replace the four plane values they came
+      // from); only the scratch writes below run under the half mask
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const uint32_t t0 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x05010400u);
+        const uint32_t t1 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x07030602u);
+        const uint32_t t2 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x05010400u);
+        const uint32_t t3 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x07030602u);
+        xl[0][i] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+        xl[1][i] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+        xl[2][i] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+        xl[3][i] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+      }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           __builtin_amdgcn_wave_barrier();
-          if ((l >> 5) == (uint32_t)h) {  // (transposes under the half mask: no registers held)
+          if ((l >> 5) == (uint32_t)h) {
             const uint32_t row = l & 31;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
               const int i = 8 * u + j;
-              const uint32_t t0 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x05010400u);
-              const uint32_t t1 = __builtin_amdgcn_perm(xl[1][i], xl[0][i], 0x07030602u);
-              const uint32_t t2 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x05010400u);
-              const uint32_t t3 = __builtin_amdgcn_perm(xl[3][i], xl[2][i], 0x07030602u);
-              *(v4u*)(wsp + 4 * (8 * row + (j ^ (row & 7)))) =
-                  v4u{__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
-                      __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
+              *(v4u*)(wsp + 4 * (8 * row + (j ^ (row & 7)))) = v4u{xl[0][i], xl[1][i], xl[2][i], xl[3][i]};
             }
           }
           __builtin_amdgcn_wave_barrier();
@@ -675,7 +726,8 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       }
       ok_tiles++;
       ok_bytes += cur.os;
-      if (threadIdx.x == 0 && kp.status) kp.status[cur.t] = TDBG_OK;
+      // (chunk mode: the directory pass wrote the tile's status)
+      if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
     }
     cur = nxt;
     cur_dma = nxt_dma;
@@ -684,9 +736,13 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
   }
   pc.flush();
   if (kp.stats && threadIdx.x == 0 && ok_tiles) {
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
+    if (chunked) {  // (the directory pass counted the tiles)
+      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
+    } else {
+      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
+      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
+      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
+    }
   }
 }
 

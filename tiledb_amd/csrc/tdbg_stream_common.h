@@ -42,17 +42,41 @@ struct Batch {
   uint32_t fs, os;  // saturated at 2^32 - 1 (such a tile fits no streaming kernel)
   uint64_t in, out;
 };
+// Chunk mode (kp.chunks set: a chunk-parallel launch, tdbg_chunkdir.hip):
+// the work items are the records of the device chunk directory, and a
+// descriptor is one chunk: its image starts at the chunk's 12-byte header
+// ([u32 orig][u32 filtered][u32 md], tile.cc:280-313) and its output at the
+// chunk's offset in the tile's buffer.
 __device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl) {
   const uint64_t j = blockIdx.x + (base + (threadIdx.x & 63)) * (uint64_t)gridDim.x;
   Batch b{0, 0, 0, 0};
   if (j < ntl) {
-    const uint64_t fs = kp.in_size[j], os = kp.out_size[j];
-    b.fs = fs < 0xffffffffull ? (uint32_t)fs : 0xffffffffu;
-    b.os = os < 0xffffffffull ? (uint32_t)os : 0xffffffffu;
-    b.in = (uint64_t)kp.in[j];
-    b.out = (uint64_t)kp.out[j];
+    if (kp.chunks) {
+      const ChunkRec r = kp.chunks[j];
+      const uint64_t fs = 12ull + r.ml + r.fl;
+      b.fs = fs < 0xffffffffull ? (uint32_t)fs : 0xffffffffu;
+      b.os = r.orig;
+      b.in = (uint64_t)kp.in[r.tile] + r.in_off - 12;
+      b.out = (uint64_t)kp.out[r.tile] + r.out_off;
+    } else {
+      const uint64_t fs = kp.in_size[j], os = kp.out_size[j];
+      b.fs = fs < 0xffffffffull ? (uint32_t)fs : 0xffffffffu;
+      b.os = os < 0xffffffffull ? (uint32_t)os : 0xffffffffu;
+      b.in = (uint64_t)kp.in[j];
+      b.out = (uint64_t)kp.out[j];
+    }
   }
   return b;
+}
+
+// work items of a launch: tiles, or (chunk mode / a queue) a device count
+__device__ __forceinline__ uint64_t work_items(const KParams& kp) {
+  uint64_t ntl = kp.ntiles;
+  if (kp.ntiles_dev) {
+    const uint64_t c = (uint32_t)__builtin_amdgcn_readfirstlane(*kp.ntiles_dev);
+    ntl = c < ntl ? c : ntl;
+  }
+  return ntl;
 }
 // (the builtin returns int: each half goes through uint32_t, or the low half
 // of a pointer would be sign-extended over the high one)

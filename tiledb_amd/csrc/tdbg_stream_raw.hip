@@ -129,7 +129,7 @@ __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
   if (threadIdx.x == 0) {
     const uint32_t k = atomicAdd(kp.sq, 1u);
     if (k < kp.sq_cap) kp.sq[1 + k] = (uint32_t)t;
-    else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
+    else if (kp.status) kp.status[kp.chunks ? kp.chunks[t].tile : t] = TDBG_E_INTERNAL;
   }
 }
 
@@ -145,14 +145,18 @@ __device__ __forceinline__ void prefix_dma(Lds& L, const Desc& d, uint32_t w, ui
 // header parse (wave 0): tile/chunk header, window table, frame, DD headers
 // ---------------------------------------------------------------------------
 template <bool SGN>
-__device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l) {
+__device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool chunked) {
   const uint32_t* P = L.PF;
+  // the chunk header follows the tile's u64 chunk count, or (chunk mode:
+  // a chunk of a multi-chunk tile) starts the image
+  const uint32_t ho = chunked ? 0u : 8u;
   const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
-  const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + 8), fl = rd32(P, b + 12),
-                 ml = rd32(P, b + 16);
-  const uint32_t m = b + 20;
+  const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + ho), fl = rd32(P, b + ho + 4),
+                 ml = rd32(P, b + ho + 8);
+  const uint32_t m = b + ho + 12;
   const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4);
-  bool ok = nlo == 1 && nhi == 0 && orig == OUTB && (uint64_t)ml + fl + 20 <= d.fs && nwr >= 2 && nwr <= TABN &&
+  bool ok = (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= d.fs && nwr >= 2 &&
+            nwr <= TABN &&
             ml == 8 + 9 * nwr + 24 && Lb == LBWR;
   const uint32_t nwin = ok ? nwr : 2;
   // lane l: windows 5l..5l+4 = 45 bytes at e0 (inside PF: m + 8 + 9 * 320 < 4096 - 64)
@@ -184,7 +188,7 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l) {
   const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
   const uint32_t inc = wave_incscan_u32(s5);
   ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
-  const uint32_t dst = 20 + ml;  // image offset of the BWR data
+  const uint32_t dst = ho + 12 + ml;  // image offset of the BWR data
   {
     uint32_t off = dst + inc - s5;
 #pragma unroll
@@ -446,7 +450,8 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
   __shared__ Lds L;
   const uint32_t w = wave_(), l = lane_();
   Walk wk{};
-  wk.ntl = kp.ntiles;
+  wk.ntl = work_items(kp);
+  const bool chunked = kp.chunks != nullptr;
   wk.base = 0;
   wk.loaded = false;
   uint64_t it = 0;
@@ -479,7 +484,7 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
     if (ABL != 1 || ok_tiles == 0) {
       if (!pf_waited) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();  // B1: the prefix has landed; the last tile's jobs are done with TAB
-      if (w == 0) parse<SGN>(L, cur, l);
+      if (w == 0) parse<SGN>(L, cur, l, chunked);
       lds_barrier();  // B2: window table and verdict
     }
     const bool ok = __builtin_amdgcn_readfirstlane(L.hd[0]) != 0;
@@ -491,14 +496,16 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
       if (ABL != 4) tile_jobs<SGN, ABL>(L, cur, w, l, wsh);
       pf_waited = true;  // the first job's wait covered the prefix (older)
       ok_tiles++;
-      if (threadIdx.x == 0 && kp.status) kp.status[cur.t] = TDBG_OK;
+      if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
     } else {
       decline(kp, cur.t);
     }
     cur = nxt;
     have = hn;
   }
-  if (kp.stats && threadIdx.x == 0 && ok_tiles) {
+  if (kp.stats && threadIdx.x == 0 && ok_tiles && chunked) {
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
+  } else if (kp.stats && threadIdx.x == 0 && ok_tiles) {
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)(ok_tiles * OUTB));
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);

@@ -296,7 +296,7 @@ __device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, ui
     const uint32_t k = b0 + (uint32_t)__builtin_popcountll(mask & ((1ull << l) - 1));
     const uint32_t t = (uint32_t)(blockIdx.x + (uint64_t)(base + l) * gridDim.x);
     if (k < kp.sq_cap) kp.sq[1 + k] = t;
-    else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
+    else if (kp.status) kp.status[kp.chunks ? kp.chunks[t].tile : t] = TDBG_E_INTERNAL;
   }
 }
 
@@ -314,9 +314,13 @@ template <int MODE, bool SGN>
 __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel(const KParams kp) {
   __shared__ Lds<MODE> L;
   const uint64_t G = gridDim.x;
-  uint64_t ntl = kp.ntiles;
+  // work items: tiles, or (chunk mode, tdbg_stream_common.h) the records of
+  // the device chunk directory
+  const uint64_t ntl = work_items(kp);
+  const bool chunked = kp.chunks != nullptr;
   // the fused kernel's fallback queue starts empty for this launch (it runs
-  // next on the same stream and is the only one to append)
+  // next on the same stream and is the only one to append; chunk mode: the
+  // host cleared it before the directory pass)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const uint32_t w = wave_();
   uint64_t ok_tiles = 0;
@@ -359,10 +363,12 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
       const uint32_t* C = L.C;
       const uint32_t b = (uint32_t)((uintptr_t)cur.in & 15);
       // ---- tile + chunk header (Tile::load_chunk_data, tile.cc:280-313) ----
-      const uint32_t nlo = c32(C, b), nhi = c32(C, b + 4), orig = c32(C, b + 8), fl = c32(C, b + 12),
-                     ml = c32(C, b + 16);
-      const uint32_t m = b + 20;
-      ok = ok && nlo == 1 && nhi == 0 && orig == OUTB && (uint64_t)ml + fl + 20 <= cur.fs;
+      // (chunk mode: the image starts at the chunk header, no u64 chunk count)
+      const uint32_t ho = chunked ? 0u : 8u;
+      const uint32_t nlo = c32(C, b), nhi = c32(C, b + 4), orig = c32(C, b + ho), fl = c32(C, b + ho + 4),
+                     ml = c32(C, b + ho + 8);
+      const uint32_t m = b + ho + 12;
+      ok = ok && (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= cur.fs;
       hd.dst = m + ml;
       if constexpr (MODE == M_DD || MODE == M_RLE) {
         // compression frame (compression_filter.cc:413-486): 0 md parts, one
@@ -641,13 +647,15 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
     if (!issued) next_dma();
     if (ok) {
       ok_tiles++;
-      if (threadIdx.x == 0 && kp.status) kp.status[cur.t] = TDBG_OK;
+      if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
     }
     cur = nxt;
     cur_dma = nxt_dma;
     stored = ok;
   }
-  if (kp.stats && threadIdx.x == 0 && ok_tiles) {
+  if (kp.stats && threadIdx.x == 0 && ok_tiles && chunked) {
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
+  } else if (kp.stats && threadIdx.x == 0 && ok_tiles) {
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)(ok_tiles * OUTB));
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);

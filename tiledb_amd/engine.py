@@ -299,6 +299,12 @@ class Context:
         _check(lib.tdbg_context_forward_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_forward_stream_stats")
         return int(n.value)
 
+    def stream_chunks(self):
+        """Chunks of chunk-parallel launches the streaming kernels took, cumulative."""
+        n = ctypes.c_uint64()
+        _check(lib.tdbg_context_stream_chunk_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_chunk_stats")
+        return int(n.value)
+
     def stream_raw_tiles(self):
         """Of those, the tiles the raw-DoubleDelta streaming kernel took, cumulative."""
         n = ctypes.c_uint64()
@@ -429,6 +435,65 @@ class Context:
                "tdbg_dense_copy_async")
 
 
+def _ptrs(xs):
+    return np.array([0 if x is None else int(x) for x in xs], dtype=np.uint64)
+
+
+def dense_copy_fragments_async(ctx, fcfg, ntiles: int, d_tile_start, d_frag_dom, d_tiles, d_fill, d_result,
+                               d_validity=None, d_result_validity=None, stream=None) -> None:
+    """tdbg_dense_copy_fragments_async on device pointers (ints)."""
+    _check(lib.tdbg_dense_copy_fragments_async(ctx.h, ctypes.byref(fcfg), ntiles, d_tile_start, d_frag_dom, d_tiles,
+                                               d_validity, d_fill, d_result, d_result_validity,
+                                               ctx._stream(stream)), "tdbg_dense_copy_fragments_async")
+
+
+def dense_var_offsets_async(ctx, fcfg, ntiles: int, d_tile_start, d_frag_dom, d_off_tiles, d_var_tiles, d_fill,
+                            d_result_offsets, d_var_total, d_validity=None, d_result_validity=None,
+                            stream=None) -> None:
+    _check(lib.tdbg_dense_var_offsets_async(ctx.h, ctypes.byref(fcfg), ntiles, d_tile_start, d_frag_dom, d_off_tiles,
+                                            d_var_tiles, d_validity, d_fill, d_result_offsets, d_result_validity,
+                                            d_var_total, ctx._stream(stream)), "tdbg_dense_var_offsets_async")
+
+
+def dense_var_copy_async(ctx, fcfg, d_result_offsets, d_var_total, d_result_var, stream=None) -> None:
+    _check(lib.tdbg_dense_var_copy_async(ctx.h, ctypes.byref(fcfg), d_result_offsets, d_var_total, d_result_var,
+                                         ctx._stream(stream)), "tdbg_dense_var_copy_async")
+
+
+def dense_read_var_host(ctx, dp_off: DevicePipeline, dp_var: DevicePipeline, fcfg, tile_start, frag_dom,
+                        off_filtered, var_filtered, var_unfiltered_size, fill_value: bytes, var_cap: int):
+    """tdbg_dense_read_var_host: host filtered offsets / var tiles per (tile,
+    fragment) (None: absent) -> (result offsets uint64, var bytes, statuses)."""
+    ntiles = len(tile_start)
+    nf = fcfg.nfrag
+    assert len(off_filtered) == ntiles * nf == len(var_filtered) == len(var_unfiltered_size)
+    keep = [np.ascontiguousarray(b, dtype=np.uint8) if b is not None else None for b in off_filtered + var_filtered]
+    op = _ptrs([None if b is None else b.ctypes.data for b in keep[:ntiles * nf]])
+    vp = _ptrs([None if b is None else b.ctypes.data for b in keep[ntiles * nf:]])
+    osz = np.array([0 if b is None else b.size for b in keep[:ntiles * nf]], dtype=np.uint64)
+    vsz = np.array([0 if b is None else b.size for b in keep[ntiles * nf:]], dtype=np.uint64)
+    vus = np.ascontiguousarray(var_unfiltered_size, dtype=np.uint64)
+    ts = np.ascontiguousarray(tile_start, dtype=np.int64).reshape(-1)
+    fd = np.ascontiguousarray(frag_dom, dtype=np.int64).reshape(-1)
+    fill = np.frombuffer(bytes(fill_value) or b"\0", dtype=np.uint8)
+    ncell = 1
+    for d in range(fcfg.base.dim_num):
+        ncell *= fcfg.base.sub_hi[d] - fcfg.base.sub_lo[d] + 1
+    roff = np.zeros(ncell, dtype=np.uint64)
+    rvar = np.zeros(max(var_cap, 1), dtype=np.uint8)
+    total = ctypes.c_uint64()
+    st = np.zeros(max(ntiles * nf, 1), dtype=np.int32)
+    rc = lib.tdbg_dense_read_var_host(ctx.h, dp_off.h, dp_var.h, ctypes.byref(fcfg), ntiles, ts.ctypes.data,
+                                      fd.ctypes.data, op.ctypes.data, osz.ctypes.data, vp.ctypes.data,
+                                      vsz.ctypes.data, vus.ctypes.data, fill.ctypes.data, roff.ctypes.data,
+                                      rvar.ctypes.data, var_cap, ctypes.byref(total),
+                                      st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    if rc and (rc in CALL_ERRORS or not st[:ntiles * nf].any()):
+        _check(rc, "tdbg_dense_read_var_host")
+    return rc, roff, bytes(rvar[:int(total.value) * (fcfg.data_type_size if fcfg.elements_mode else 1)]), \
+        st[:ntiles * nf]
+
+
 def unfilter_cpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, nthreads: int = 0,
                  offsets_tiles: bool = False) -> np.ndarray:
     """tdbg_unfilter_tiles_cpu: host tiles -> host outputs on nthreads host
@@ -536,6 +601,17 @@ def dense_config(cell_size: int, tile_extent, sub_lo, sub_hi, cell_order: int = 
     for d in range(nd):
         g.tile_extent[d], g.sub_lo[d], g.sub_hi[d] = int(tile_extent[d]), int(sub_lo[d]), int(sub_hi[d])
     return g
+
+
+def dense_frag_config(cell_size: int, tile_extent, sub_lo, sub_hi, nfrag: int, fill_size: int, cell_order: int = 0,
+                      layout: int = 0, nullable: bool = False, fill_validity: int = 0, elements_mode: bool = False,
+                      data_type_size: int = 1) -> "_native.DenseFragConfig":
+    """tdbg_dense_frag_config: several fragments (the lower index wins), fill values, var cells."""
+    f = _native.DenseFragConfig()
+    f.base = dense_config(cell_size, tile_extent, sub_lo, sub_hi, cell_order, layout)
+    f.nfrag, f.nullable, f.fill_size, f.fill_validity = nfrag, int(nullable), fill_size, fill_validity
+    f.elements_mode, f.data_type_size = int(elements_mode), data_type_size
+    return f
 
 
 def dense_result_bytes(cfg) -> int:
