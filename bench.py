@@ -315,7 +315,10 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
                         stream_chunks=schunks,
                         packed=packed, offs=offs, sizes=sizes, steps=steps, ntiles=ntiles)
         if forward and vi == 0 and not ablation and cfgname != "fscale":  # (lossy: values differ)
-            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx, pool, steps, warmup, dist)
+            # (on at most one GPU's shard of C5, 12,500 tiles: the forward leg
+            # checks every filtered tile against the encoder's bytes on the host)
+            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx[: args.shard_tiles or ntiles], pool, steps,
+                                           warmup, dist)
         if e2e_leg:
             ne = min(ntiles, args.e2e_tiles) if args.e2e_tiles else ntiles
             res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs[:ne], sizes[:ne], int(vals[0].nbytes), args, dist,
@@ -323,6 +326,54 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
         del batch
         torch.cuda.empty_cache()
     return dp, res
+
+
+def c3_combined(engine, ctx, W, args):
+    """the literal [DOUBLE_DELTA, RLE] cannot be built (DESIGN
+    7), so C3a [DOUBLE_DELTA] and C3b [RLE] run back to back on the same
+    coordinates: one step = the C3a launch then the C3b launch on one stream,
+    both batches resident.  Combined rate = both launches' unfiltered bytes /
+    the step's wall time; frac = both launches' B_alg / their kernels' time
+    (HIP events on the launch stream)."""
+    import torch
+    parts = []
+    for c in ("c3a", "c3b"):
+        ser, dt, cs, _, _ = W.config(c)
+        dp = engine.DevicePipeline(ser, 23, int(dt), cs)
+        batch, pool, vals, idx, packed, offs, sizes = build_batch(
+            engine, c, "coords", CONFIGS[c]["tiles_per_gpu"], args.unique, torch.cuda.current_device(), seed=5,
+            ctx=ctx, dp=dp)
+        if ctx.unfilter(dp, batch).any():
+            raise SystemExit(f"{c}: first pass status nonzero")
+        parts.append((c, dp, batch, vals, idx, float(sizes.sum()), float(sum(vals[i].nbytes for i in idx))))
+    stream = torch.cuda.current_stream()
+    for _ in range(max(1, args.warmup)):
+        for _, dp, batch, *_ in parts:
+            ctx.unfilter_async(dp, batch, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    ctx.time_launches(2 * args.steps)
+    for p_ in parts:
+        p_[2].d_status.fill_(-1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for _, dp, batch, *_ in parts:
+            ctx.unfilter_async(dp, batch, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern_ms, _ = ctx.launch_times(2 * args.steps)
+    for c, dp, batch, vals, idx, _, _ in parts:
+        if batch.d_status[: batch.ntiles].cpu().numpy().any():
+            raise SystemExit(f"{c}: timed launches: device status nonzero")
+        verify(batch, vals, idx)
+    unf = sum(p_[6] for p_ in parts)
+    b_alg = sum(p_[5] + p_[6] for p_ in parts)
+    k_ms = float(np.sum(kern_ms)) / args.steps
+    return {"workload": "C3a [DOUBLE_DELTA] then C3b [RLE] on the same uint64 coordinates, back to back on one "
+                        "stream (10,000 tiles each)",
+            "GiBps": round(unf / (el / args.steps) / 2**30, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
+            "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_step": int(b_alg),
+            "roofline_frac": round(b_alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def gibps(r, world):
@@ -461,6 +512,7 @@ def headline_line(args, W, variants, res, world):
         line["forward"] = {
             "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
             "variant": fv,
+            "tiles_per_gpu": int(round(fin / r["out_bytes"])),
             "value": round(fin * world / (el / r["steps"]) / 2**30, 2),
             "unit": "GiB/s",
             "ms_per_step": round(el / r["steps"] * 1e3, 4),
@@ -585,6 +637,7 @@ def main():
             for v in cres:  # free the host copies
                 cres[v].pop("packed", None)
         line["config"]["other_configs"] = others
+        line["config"]["c3_combined"] = c3_combined(engine, ctx, W, args)
         # C5 on one GPU's shard of the 8-GPU config (12,500 tiles): the
         # per-GPU work of the N = 8 line
         if args.shard_tiles and args.shard_tiles != ntiles:

@@ -115,6 +115,31 @@ def test_double_delta_reinterpret_byte_by_version(native):
     assert dp.num_filters == 1 and dp.supported
 
 
+def test_filtered_bound_follows_the_compressor(native):
+    """A compression filter runs the stage its compressor names
+    (compression_filter.cc: the filter type is the compressor's), and so does
+    tdbg_filtered_bound: a GZIP-typed filter carrying DOUBLE_DELTA is bounded
+    as DOUBLE_DELTA, a DOUBLE_DELTA-typed one with compressor NONE as no stage."""
+    from tiledb_amd import _native
+    from tiledb_amd.engine import DevicePipeline
+    hdr = struct.pack("<II", 65536, 1)
+    dd = hdr + struct.pack("<BIBiB", int(FilterType.FILTER_DOUBLE_DELTA), 6, int(Compressor.DOUBLE_DELTA), -1,
+                           int(Datatype.ANY))
+    gz_dd = hdr + struct.pack("<BIBi", int(FilterType.FILTER_GZIP), 5, int(Compressor.DOUBLE_DELTA), -1)
+    dd_none = hdr + struct.pack("<BIBiB", int(FilterType.FILTER_DOUBLE_DELTA), 6, int(Compressor.NO_COMPRESSION),
+                                -1, int(Datatype.ANY))
+    empty = struct.pack("<II", 65536, 0)
+
+    def bound(ser):
+        dp = DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+        assert dp.supported
+        return [_native.lib.tdbg_filtered_bound(dp.h, n, 65536) for n in (4, 65536, 1 << 22)]
+
+    assert bound(gz_dd) == bound(dd)
+    assert bound(dd_none) == bound(empty)
+    assert all(a > b for a, b in zip(bound(dd), bound(empty)))
+
+
 def test_shard_tiles_balanced_and_covering(native):
     from tiledb_amd.engine import shard_tiles
     rng = np.random.default_rng(1)

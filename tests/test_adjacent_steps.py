@@ -246,6 +246,30 @@ def test_dense_read_fused_copy(oracle_mod, case):
 
 
 @pytest.mark.gpu
+def test_dense_read_rejects_uncovered_subarray():
+    """tdbg_dense_read_host has no fill value: a tile set that leaves result
+    cells uncovered (a missing tile, a tile given twice, a start off the tile
+    grid) is an argument error, and the result buffer is left untouched."""
+    from tiledb_amd import engine
+    rng = np.random.default_rng(77)
+    ext, shape_tiles, lo, hi = (16, 32), (3, 3), (2, 5), (40, 90)
+    _, raw, starts = _dense_tiles(shape_tiles, ext, 0, rng)
+    ser = FilterPipeline(65536, [ByteshuffleFilter()]).serialize()
+    ctx = engine.Context(0)
+    dp = engine.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+    cfg = engine.dense_config(4, ext, lo, hi, 0, 0)
+    nb = engine.dense_result_bytes(cfg)
+    off = starts.copy()
+    off[4] += (1, 0)
+    for tiles, st in ((raw[:-1], starts[:-1]), (raw + raw[:1], np.vstack([starts, starts[:1]])), (raw, off)):
+        result = np.full(nb, 0xAB, dtype=np.uint8)
+        with pytest.raises(engine.EngineError) as ei:
+            ctx.dense_read(dp, tiles, st, cfg, result)
+        assert ei.value.code == 1  # TDBG_E_ARG
+        assert (result == 0xAB).all()
+
+
+@pytest.mark.gpu
 def test_dense_copy_async_skips_failed_tiles(oracle_mod):
     """Device-resident copy: a tile whose status is not OK leaves its cells
     untouched; the others land where copy_fixed_tiles puts them."""

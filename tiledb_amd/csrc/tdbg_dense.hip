@@ -11,9 +11,9 @@
 // with the tile-side stride.  Here one workgroup takes a tile, computes the
 // tile's intersection with the subarray, and copies it: slab-wise with
 // 16/4/1-byte vectors (same order) or cell-wise (transposing order), into
-// the device result buffer.  Scope: one fragment covering the subarray, one
-// range per dimension, fixed-size cells -- the single-fragment dense read;
-// several overlapping fragments and fill values stay in the reader.
+// the device result buffer.  Scope of this first kernel: one fragment
+// covering the subarray, one range per dimension, fixed-size cells; several
+// fragments, fill values and var-sized cells follow below.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -988,6 +988,9 @@ uint64_t tdbg_filtered_bound(const tdbg_pipeline* p, uint64_t tile_size, uint32_
   uint64_t D = chunk, M = 0, MP = 0;  // data bytes, metadata bytes, metadata buffers
   for (const Filter& f : p->filters) {
     const uint64_t ts = dt_size(f.datatype);
+    // (f.type of a compression filter is the one its compressor names,
+    // resolved at parse time: a GZIP-typed filter carrying DOUBLE_DELTA is a
+    // DOUBLE_DELTA stage here, one with compressor NONE a NONE stage)
     switch (f.type) {
       case TDBG_FILTER_BYTESHUFFLE: case TDBG_FILTER_BITSHUFFLE: case TDBG_FILTER_XOR:
         M += 4 + 8 * kParts;
@@ -1717,6 +1720,31 @@ int tdbg_dense_read_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntile
   if (!result || result_size < rbytes) return fail(TDBG_E_ARG, "result buffer smaller than the subarray");
   if (ntiles == 0) return TDBG_OK;
   if (!in || !in_size || !tile_start) return fail(TDBG_E_ARG, "null tile arrays");
+  {
+    // Every result cell must come from a tile (this entry has no fill value,
+    // and the device result buffer is not initialised): the tiles lie on one
+    // grid (tile 0's start as origin), are distinct, and their intersections
+    // with the subarray add up to the whole subarray.
+    const uint32_t nd = cfg->dim_num;
+    uint64_t want = 1, got = 0;
+    for (uint32_t d = 0; d < nd; d++) want *= (uint64_t)(cfg->sub_hi[d] - cfg->sub_lo[d] + 1);
+    std::vector<std::vector<int64_t>> keys(ntiles);
+    for (uint64_t t = 0; t < ntiles; t++) {
+      uint64_t n = 1;
+      for (uint32_t d = 0; d < nd; d++) {
+        const int64_t s = tile_start[t * nd + d], e = cfg->tile_extent[d];
+        if ((s - tile_start[d]) % e != 0) return fail(TDBG_E_ARG, "dense read: tile start off the tile grid");
+        const int64_t lo = std::max(s, cfg->sub_lo[d]), hi = std::min(s + e - 1, cfg->sub_hi[d]);
+        n = hi < lo ? 0 : n * (uint64_t)(hi - lo + 1);
+      }
+      got += n;
+      keys[t].assign(tile_start + t * nd, tile_start + (t + 1) * nd);
+    }
+    std::sort(keys.begin(), keys.end());
+    if (std::adjacent_find(keys.begin(), keys.end()) != keys.end())
+      return fail(TDBG_E_ARG, "dense read: a tile is given twice");
+    if (got != want) return fail(TDBG_E_ARG, "dense read: the tiles do not cover the subarray");
+  }
   HIP_OK(hipSetDevice(c->device));
   if (batch_bytes == 0) batch_bytes = 256ull << 20;
   const bool cin = (flags & TDBG_HOST_CONTIGUOUS_INPUT) != 0;
