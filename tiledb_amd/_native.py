@@ -128,8 +128,17 @@ class DenseFragConfig(ctypes.Structure):
                 ("fill_size", ctypes.c_uint32), ("fill_validity", ctypes.c_uint32),
                 ("elements_mode", ctypes.c_uint32), ("data_type_size", ctypes.c_uint32)]
 
+# symbols an older experimental build (TDBG_LIB) lacks; the product library
+# must export every one
+MISSING: set = set()
 for _name, (_res, _args) in SIGNATURES.items():
-    _f = getattr(lib, _name)
+    try:
+        _f = getattr(lib, _name)
+    except AttributeError:
+        if not os.environ.get("TDBG_LIB"):
+            raise
+        MISSING.add(_name)
+        continue
     _f.restype = _res
     _f.argtypes = _args
 

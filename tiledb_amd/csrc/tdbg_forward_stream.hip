@@ -125,11 +125,6 @@ __device__ __forceinline__ void lds_u32b(Lds& L, uint32_t o, uint32_t v) {
   for (int i = 0; i < 4; i++) lds_byte(L, o + i, v >> (8 * i));
 }
 
-template <bool SGN>
-__device__ __forceinline__ int64_t ext32(uint32_t v) {
-  return SGN ? (int64_t)(int32_t)v : (int64_t)v;
-}
-__device__ __forceinline__ uint64_t uabs(int64_t v) { return v < 0 ? 0ull - (uint64_t)v : (uint64_t)v; }
 
 // Reductions over a 16-lane DPP row (the lanes of one BWR window, or a
 // wave's row): quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
@@ -160,6 +155,81 @@ __device__ __forceinline__ uint64_t row_max64(uint64_t v) {
   step(((uint64_t)dpp_<0x141>((uint32_t)(v >> 32)) << 32) | dpp_<0x141>((uint32_t)v));
   step(((uint64_t)dpp_<0x140>((uint32_t)(v >> 32)) << 32) | dpp_<0x140>((uint32_t)v));
   return v;
+}
+
+// DoubleDelta codes of thread T's four runs (plane k: positions 8T..8T+7,
+// i.e. S[2..9][k]) at compile-time code width CB = bitsize + 1
+// (dd_compressor.cc:243-257, 406-450: a sign bit, then bitsize magnitude bits, MSB
+// first from bit 63 of little-endian u64 words).  A run's 8 codes are one
+// contiguous bit range: they are packed at compile-time bit positions into 8
+// run dwords R (MSB first), then shifted to the run's stream bit offset with
+// one v_alignbit per output chunk.  Chunk c of the stream (32 bits, stream
+// order) is LDS dword WD0 + (c ^ 1) (the high half of a u64 word comes
+// first).  Chunks wholly inside the run are plain writes; the first and the
+// last one or two are shared with the neighbouring runs and OR-ed (the
+// region was zeroed before B1).  Thread 0's plane-0 run has codes from
+// position 2 only: it is packed with two zero codes in front at stream bit
+// -2 CB and its chunks below 0 are not written.
+template <int CB>
+__device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint32_t T) {
+  constexpr uint32_t BS = CB - 1;            // bitsize
+  constexpr int JF = (8 * CB) / 32 - 1;      // chunks 1..JF lie inside the run for any start bit
+  constexpr int JX = (8 * CB + 30) / 32;     // the last chunk a run can reach
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t code[8];
+    uint32_t dprev = S[1][k] - S[0][k];
+#pragma unroll
+    for (int i = 2; i < 10; i++) {
+      // (coded: |dd| < 2^30, so the wrapped 32-bit value is exact)
+      const uint32_t d = S[i][k] - S[i - 1][k];
+      const int32_t dd = (int32_t)(d - dprev);
+      dprev = d;
+      const uint32_t a = (uint32_t)(dd < 0 ? -dd : dd);
+      code[i - 2] = (((uint32_t)dd >> 31) << BS) | a;
+    }
+    const bool t0 = k == 0 && T == 0;
+    if (k == 0) {
+      code[0] = t0 ? 0u : code[0];
+      code[1] = t0 ? 0u : code[1];
+    }
+    uint32_t R[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) R[j] = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int off = j * CB, w0 = off >> 5, sh = off & 31;
+      if (sh + CB <= 32) {
+        R[w0] |= code[j] << (32 - sh - CB);
+      } else {
+        R[w0] |= code[j] >> (sh + CB - 32);
+        R[w0 + 1] |= code[j] << (64 - sh - CB);
+      }
+    }
+    // stream bit of the run's first code (code index 4096 k + 8 T - 2)
+    const int32_t B0 = ((int32_t)(4096 * k) + 8 * (int32_t)T - 2) * CB;
+    const int32_t c0 = B0 >> 5;
+    const uint32_t nb0 = (uint32_t)B0 & 31u;
+    const int32_t base = (int32_t)WD0 + (c0 & ~1);
+    const uint32_t par = (uint32_t)c0 & 1u;
+    // dword of chunk c0 + j: base + ((j + par) ^ 1), i.e. (even j) base + 1 - par + j,
+    // (odd j) base - 1 + 3 par + j
+    uint32_t* const pe = L.B + (base + 1 - (int32_t)par);
+    uint32_t* const po = L.B + (base - 1 + 3 * (int32_t)par);
+    const int32_t jmax = (int32_t)((8 * CB - 1 + nb0) >> 5);
+#pragma unroll
+    for (int j = 0; j <= JX; j++) {
+      const uint32_t hi = j == 0 ? 0u : R[j - 1], lo = j == 8 ? 0u : R[j];
+      const uint32_t ch = __builtin_amdgcn_alignbit(hi, lo, nb0);
+      uint32_t* const dst = (j & 1 ? po : pe) + j;
+      const bool inside = k != 0 || c0 + j >= 0;  // (thread 0, plane 0: no chunks below 0)
+      if (j >= 1 && j <= JF) {
+        if (inside) *dst = ch;
+      } else if (j <= jmax && inside) {
+        atomicOr(dst, ch);
+      }
+    }
+  }
 }
 
 template <bool SGN>
@@ -230,7 +300,11 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           const uint32_t P = 4096 * k + 8 * T + i - 2;
           const double x = f(S[i][k]);
           const double d = x - x1, dp = x1 - x2;
-          const double a = P >= 2 ? __builtin_fabs(d - dp) : P == 1 ? __builtin_fabs(d) : 0.0;
+          double a = __builtin_fabs(d - dp);
+          // (only positions 0 and 1 -- thread 0, plane 0 -- differ: no dd
+          // there, and d1 counts for position 1; a compile-time guard keeps
+          // the selects off every other value)
+          if (k == 0 && i < 4) a = P >= 2 ? a : P == 1 ? __builtin_fabs(d) : 0.0;
           mxd = __builtin_fmax(mxd, a);
           x2 = x1;
           x1 = x;
@@ -280,38 +354,18 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           L.B[(DELTA + 26) / 4] = S[2][0];
           L.B[(DELTA + 30) / 4] = S[3][0];
         }
-        // A run (plane k) is 8 consecutive codes = one contiguous bit range:
-        // its codes are shifted into a 64-bit accumulator and every whole
-        // 32-bit chunk leaves as it fills -- plain stores for the chunks the
-        // run owns, ds_or only for its first and last chunk (shared with the
-        // neighbouring runs; the region was zeroed before B1).
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const uint32_t P0 = 4096 * k + 8 * T;
-          const uint32_t i0 = P0 < 2 ? 2 + (2 - P0) : 2;  // (T = 0, k = 0: codes from position 2)
-          const uint32_t bp0 = ((P0 < 2 ? 2 : P0) - 2) * cb;
-          uint32_t c = bp0 >> 5, nb = bp0 & 31;  // chunk being filled, bits already in it
-          uint64_t acc = 0;
-          bool first = true;
-#pragma unroll
-          for (int i = 2; i < 10; i++) {
-            if ((uint32_t)i < i0) continue;
-            // (coded: |dd| < 2^30, so the wrapped 32-bit value is exact)
-            const int32_t dd = (int32_t)(S[i][k] - 2u * S[i - 1][k] + S[i - 2][k]);
-            const uint32_t code = (dd < 0 ? 1u << bitsize : 0u) | (uint32_t)(dd < 0 ? -dd : dd);
-            acc = (acc << cb) | code;  // low nb + cb <= 63 bits pending
-            nb += cb;
-            if (nb >= 32) {
-              const uint32_t chunk = (uint32_t)(acc >> (nb - 32));
-              if (first) atomicOr(&L.B[WD0 + (c ^ 1)], chunk);
-              else L.B[WD0 + (c ^ 1)] = chunk;
-              first = false;
-              c++;
-              nb -= 32;
-              acc &= (1ull << nb) - 1;
-            }
-          }
-          if (nb) atomicOr(&L.B[WD0 + (c ^ 1)], (uint32_t)(acc << (32 - nb)));
+        // one instantiation per code width (uniform)
+        switch (__builtin_amdgcn_readfirstlane(cb)) {
+#define TDBG_FCB(c) \
+  case c: dd_emit<c>(L, S, T); break;
+          TDBG_FCB(2) TDBG_FCB(3) TDBG_FCB(4) TDBG_FCB(5) TDBG_FCB(6) TDBG_FCB(7) TDBG_FCB(8) TDBG_FCB(9)
+          TDBG_FCB(10) TDBG_FCB(11) TDBG_FCB(12) TDBG_FCB(13) TDBG_FCB(14) TDBG_FCB(15) TDBG_FCB(16)
+          TDBG_FCB(17) TDBG_FCB(18) TDBG_FCB(19) TDBG_FCB(20) TDBG_FCB(21) TDBG_FCB(22) TDBG_FCB(23)
+          TDBG_FCB(24) TDBG_FCB(25) TDBG_FCB(26) TDBG_FCB(27) TDBG_FCB(28) TDBG_FCB(29) TDBG_FCB(30)
+          TDBG_FCB(31)
+#undef TDBG_FCB
+          default:
+            break;  // (cb = bitsize + 1 is 2..31 when not raw)
         }
       }
       __syncthreads();  // B2: DD output complete
@@ -342,42 +396,40 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
             for (int e = 0; e < 8; e++) E[p][e] = __builtin_amdgcn_alignbyte(Q[e + 1], Q[e], 2);
             const uint32_t nb = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
             const uint32_t ne = nb >> 2;
-            uint32_t mn32 = SGN ? 0x7fffffffu : 0xffffffffu, mx32 = SGN ? 0x80000000u : 0u;
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-              if (8 * li + e < ne) {
-                const uint32_t v = E[p][e];
-                if (SGN) {
-                  mn32 = (int32_t)v < (int32_t)mn32 ? v : mn32;
-                  mx32 = (int32_t)v > (int32_t)mx32 ? v : mx32;
-                } else {
-                  mn32 = v < mn32 ? v : mn32;
-                  mx32 = v > mx32 ? v : mx32;
-                }
+            auto mm = [&](uint32_t v, uint32_t& mn, uint32_t& mx) {
+              if (SGN) {
+                mn = (int32_t)v < (int32_t)mn ? v : mn;
+                mx = (int32_t)v > (int32_t)mx ? v : mx;
+              } else {
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
               }
+            };
+            uint32_t mn32 = E[p][0], mx32 = E[p][0];
+            if (ne == 64) {  // every window but the last: all 8 elements count
+#pragma unroll
+              for (int e = 1; e < 8; e++) mm(E[p][e], mn32, mx32);
+            } else {
+              mn32 = SGN ? 0x7fffffffu : 0xffffffffu;
+              mx32 = SGN ? 0x80000000u : 0u;
+#pragma unroll
+              for (int e = 0; e < 8; e++)
+                if (8 * li + e < ne) mm(E[p][e], mn32, mx32);
             }
             half_minmax<SGN>(mn32, mx32);
-            const int64_t mn = ext32<SGN>(mn32), mxv = ext32<SGN>(mx32);
             if (li == 0) {
-              // compute_bits_required (bit_width_reduction_filter.cc:406-447)
+              // compute_bits_required (bit_width_reduction_filter.cc:406-447),
+              // in 32 bits: range = max - min < 2^32 is exact as a u32
+              // difference; signed: bits 32 when range > INT32_MAX or
+              // range + 1 > INT32_MAX, i.e. range >= 2^31 - 1
               uint32_t bits = 32;
               int32_t minv = 0;
               if (ne > 0) {
-                if (SGN) {
-                  const int64_t range = mxv - mn;
-                  if (!(range > 2147483647LL || range + 1 > 2147483647LL)) {
-                    const int64_t ro = range + 1;
-                    bits = ro <= 127 ? 8 : ro <= 32767 ? 16 : 32;
-                    minv = (int32_t)mn;
-                  }
-                } else {
-                  const uint64_t range = (uint64_t)mxv - (uint64_t)mn;
-                  if (range != 0xffffffffull) {
-                    const uint64_t ro = range + 1;
-                    const uint32_t nbits = 64 - __builtin_clzll(ro);
-                    bits = nbits <= 8 ? 8 : nbits <= 16 ? 16 : 32;
-                    minv = (int32_t)(uint32_t)mn;
-                  }
+                const uint32_t range = mx32 - mn32;
+                if (SGN ? range < 0x7fffffffu : range != 0xffffffffu) {
+                  const uint32_t ro = range + 1;
+                  bits = ro <= (SGN ? 127u : 255u) ? 8 : ro <= (SGN ? 32767u : 65535u) ? 16 : 32;
+                  minv = (int32_t)mn32;
                 }
               }
               const bool wraw = bits >= 32 || (nb & 3) != 0;

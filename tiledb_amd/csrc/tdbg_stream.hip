@@ -245,24 +245,16 @@ __device__ __forceinline__ void dd_codes(const uint32_t (&H)[18], uint32_t p, ui
   Bout = xrun;
 }
 
-#ifndef TDBG_H_MISALIGNED
-#define TDBG_H_MISALIGNED 1
-#endif
-typedef uint32_t u32_a2 __attribute__((aligned(2)));
-
 template <int CB>
 __device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uint32_t p, uint32_t n,
                                             bool first, uint32_t x0, uint32_t x1, uint32_t (&xl)[16],
                                             uint32_t& A, uint32_t& B) {
+  // (H[x] = the dword at byte 2 of scratch dword g + x.  One 2-byte-aligned
+  // ds_read_b32 per H[x] instead of the aligned pairs and a v_alignbyte
+  // takes 18 VALU off each plane but made the kernel 19 % slower: 0.2782-
+  // 0.2806 vs 0.2352-0.2363 ms per 12,500-tile launch, same box, same call,
+  // profiles/r04/ab2_*.json -- misaligned LDS reads are slow on gfx950)
   uint32_t H[18];
-#if TDBG_H_MISALIGNED
-  // H[x] = the dword at byte 2 of scratch dword g + x: one 2-byte-aligned
-  // ds_read_b32 each (gfx950 LDS reads any alignment) instead of aligned
-  // pairs and a v_alignbyte
-  const uint8_t* b8 = (const uint8_t*)(wsp + g) + 2;
-#pragma unroll
-  for (int x = 0; x < 18; x++) H[x] = *(const u32_a2*)(b8 + 4 * x);
-#else
   uint32_t G[20];
 #pragma unroll
   for (int x = 0; x < 10; x++) {
@@ -272,7 +264,6 @@ __device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uin
   }
 #pragma unroll
   for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
-#endif
   dd_codes<CB>(H, p, n, first, x0, x1, xl, A, B);
 }
 
@@ -433,22 +424,45 @@ __device__ __forceinline__ void plane_fold(const Lds& L, uint32_t w, uint32_t l,
   }
 }
 
-// The four planes of one tile (code width CB), each followed by one
-// workgroup barrier that publishes the (plane, wave) totals; after the first
-// one the waves' DD-header verdicts are ANDed (vok).  Exactly four barriers
-// whatever the data (the caller's default case executes four too).
+#ifndef TDBG_PLANE_BARRIERS
+#define TDBG_PLANE_BARRIERS 4
+#endif
+// The four planes of one tile (code width CB).  TDBG_PLANE_BARRIERS == 4:
+// each plane is followed by one workgroup barrier that publishes its (plane,
+// wave) totals and its fold; == 1: the four planes run back to back and one
+// barrier publishes all sixteen totals before the four folds (the lane keeps
+// its four (ae, be) prefixes).  After the first barrier the waves' DD-header
+// verdicts are ANDed (vok).  The barrier count depends only on the build
+// (the caller's default case executes as many).
 template <int CB, bool SGN>
 __device__ __forceinline__ void planes4(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
                                         uint32_t (&xl)[4][16], bool& ok, Clock& pc) {
-  uint32_t X = 0, D = 0, ae = 0, be = 0;
-  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae, be, pc);
-  sc::lds_barrier();
-  {
+  uint32_t X = 0, D = 0;
+  auto verdicts = [&] {
     uint32_t all = 1;
 #pragma unroll
     for (int v = 0; v < NWV; v++) all &= L.vok[v];
     ok = ok && all != 0;
+  };
+#if TDBG_PLANE_BARRIERS == 1
+  uint32_t ae[4], be[4];
+  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae[0], be[0], pc);
+  plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae[1], be[1], pc);
+  plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae[2], be[2], pc);
+  plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae[3], be[3], pc);
+  sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
+  verdicts();
+  if (ok) {
+    plane_fold<0>(L, w, l, X, D, ae[0], be[0], xl[0]);
+    plane_fold<1>(L, w, l, X, D, ae[1], be[1], xl[1]);
+    plane_fold<2>(L, w, l, X, D, ae[2], be[2], xl[2]);
+    plane_fold<3>(L, w, l, X, D, ae[3], be[3], xl[3]);
   }
+#else
+  uint32_t ae = 0, be = 0;
+  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae, be, pc);
+  sc::lds_barrier();
+  verdicts();
   if (ok) plane_fold<0>(L, w, l, X, D, ae, be, xl[0]);
   plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae, be, pc);
   sc::lds_barrier();
@@ -459,6 +473,7 @@ __device__ __forceinline__ void planes4(Lds& L, const Win& W, uint32_t w, uint32
   plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae, be, pc);
   sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
   if (ok) plane_fold<3>(L, w, l, X, D, ae, be, xl[3]);
+#endif
 }
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
@@ -646,7 +661,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
       TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
       TDBG_CB(31)
 #undef TDBG_CB
-      default:  // declined (ok is false): the same four barriers
+      default:  // declined (ok is false): the same barriers as planes4
         ok = false;
         // (defined values: an undefined xl here lets the register allocator
         // keep the last tile's values live around the loop)
@@ -654,10 +669,8 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
         for (int k = 0; k < 4; k++)
 #pragma unroll
           for (int i = 0; i < 16; i++) xl[k][i] = 0;
-        lds_barrier();
-        lds_barrier();
-        lds_barrier();
-        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < TDBG_PLANE_BARRIERS; k++) lds_barrier();
         break;
     }
     }  // cur_dma

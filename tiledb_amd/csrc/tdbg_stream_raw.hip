@@ -133,12 +133,15 @@ __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
   }
 }
 
-// prefix DMA: wave w moves units [64 w, 64 w + 64) of the image's first 4 KiB
-// (the image is > SMALL bytes, so all 256 units lie inside it: one
-// instruction per wave, every lane active)
+// prefix DMA: wave w < 3 moves units [64 w, 64 w + 64) of the image's first
+// 3 KiB (the image is > SMALL bytes, so all 192 units lie inside it: one
+// instruction per wave, every lane active).  The parse reads no byte past
+// m + ml + 28 <= 35 + 8 + 9 * 320 + 24 + 28 < 3 KiB - 16 (nwin <= TABN), so
+// the rest of PF may hold the last tile's bytes; staging only what the parse
+// reads keeps the re-read of window 0's data (the jobs DMA it again) small.
 __device__ __forceinline__ void prefix_dma(Lds& L, const Desc& d, uint32_t w, uint32_t l) {
   const uint64_t a0 = (uint64_t)d.in & ~15ull;
-  dma16(a0 + 16ull * (64 * w + l), lds_addr(L.PF) + 1024 * w);
+  if (w < 3) dma16(a0 + 16ull * (64 * w + l), lds_addr(L.PF) + 1024 * w);
 }
 
 // ---------------------------------------------------------------------------

@@ -301,6 +301,8 @@ class Context:
 
     def stream_chunks(self):
         """Chunks of chunk-parallel launches the streaming kernels took, cumulative."""
+        if "tdbg_context_stream_chunk_stats" in _native.MISSING:  # (an older TDBG_LIB build)
+            return 0
         n = ctypes.c_uint64()
         _check(lib.tdbg_context_stream_chunk_stats(self.h, ctypes.byref(n)), "tdbg_context_stream_chunk_stats")
         return int(n.value)
