@@ -112,6 +112,28 @@ def test_forward_rejections(eng, ctx, oracle_mod):
     assert forward_parity(eng, ctx, oracle_mod, c, roundtrip=False)[0] == 0
 
 
+def test_forward_sync_statuses_after_status_buffer_growth(eng, oracle_mod):
+    """tdbg_filter_tiles_sync on a fresh context, first with one tile, then
+    with more tiles than its status buffer holds: the buffer grows before
+    the kernel is handed its address, so the statuses read back are the ones
+    the kernel wrote (a rejected tile among them keeps its error; before the
+    fix the kernel wrote into the freed buffer and the copy read the new,
+    unwritten one)."""
+    from tests.cases import Case, P, as_u8
+    from tiledb_amd.filter_pipeline import Datatype, PositiveDeltaFilter
+    ctx = eng.Context(0)
+    good = as_u8(np.arange(1000, dtype=np.uint32))
+    bad = as_u8(np.array([5, 4, 3] * 50, dtype=np.uint32))
+    forward_parity(eng, ctx, oracle_mod, Case("pd_one", P(PositiveDeltaFilter(64)), Datatype.UINT32, 4, [good]),
+                   roundtrip=False)
+    for n in (40, 3000):
+        tiles = [good] * n
+        tiles[n // 2] = bad
+        st = forward_parity(eng, ctx, oracle_mod,
+                            Case(f"pd_{n}", P(PositiveDeltaFilter(64)), Datatype.UINT32, 4, tiles), roundtrip=False)
+        assert st[n // 2] != 0 and not np.delete(st, n // 2).any()
+
+
 def test_forward_full_size_c5(eng, ctx, oracle_mod):
     """A BASELINE C5 shard's worth of tiles (2,000 x 64 KiB, active + ramp +
     rand): forward on the device, every tile equal to the oracle's bytes and

@@ -1140,8 +1140,16 @@ int tdbg_filter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t nti
                            const uint64_t* d_out_cap, uint64_t* d_out_len, uint32_t max_chunk,
                            int32_t* host_status, tdbg_stream stream) {
   if (ntiles == 0) return TDBG_OK;
-  int rc = tdbg_filter_tiles_async(c, p, ntiles, d_in, d_in_size, d_out, d_out_cap, d_out_len, max_chunk,
-                                   c ? c->d_status : nullptr, stream);
+  if (!c) return fail(TDBG_E_ARG, "null context or pipeline");
+  // the context's status buffer is (re)sized here, before its address is
+  // taken: the async entry's own ensure_status would otherwise reallocate
+  // it after the kernel was handed the old one, and the copy below would
+  // read statuses no kernel wrote
+  HIP_OK(hipSetDevice(c->device));
+  int rc = ensure_status(c, ntiles);
+  if (rc) return rc;
+  rc = tdbg_filter_tiles_async(c, p, ntiles, d_in, d_in_size, d_out, d_out_cap, d_out_len, max_chunk,
+                               c->d_status, stream);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   std::vector<int32_t> st(ntiles);

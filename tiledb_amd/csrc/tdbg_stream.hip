@@ -424,17 +424,17 @@ __device__ __forceinline__ void plane_fold(const Lds& L, uint32_t w, uint32_t l,
   }
 }
 
-#ifndef TDBG_PLANE_BARRIERS
-#define TDBG_PLANE_BARRIERS 4
-#endif
-// The four planes of one tile (code width CB).  TDBG_PLANE_BARRIERS == 4:
+// The four planes of one tile (code width CB).  PB == 4:
 // each plane is followed by one workgroup barrier that publishes its (plane,
-// wave) totals and its fold; == 1: the four planes run back to back and one
+// wave) totals and its fold; PB == 1: the four planes run back to back and one
 // barrier publishes all sixteen totals before the four folds (the lane keeps
 // its four (ae, be) prefixes).  After the first barrier the waves' DD-header
-// verdicts are ANDed (vok).  The barrier count depends only on the build
-// (the caller's default case executes as many).
-template <int CB, bool SGN>
+// verdicts are ANDed (vok).  The barrier count depends only on PB (the
+// caller's default case executes as many).  Measured (profiles/r04/
+// barriers/): PB = 1 is 4 % faster on 12,500-tile launches (12 tiles per
+// workgroup: shorter tiles, shorter tail), PB = 4 0.8 % faster on 100,000
+// (98 per workgroup); the launcher picks by tiles per workgroup.
+template <int CB, bool SGN, int PB>
 __device__ __forceinline__ void planes4(Lds& L, const Win& W, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
                                         uint32_t (&xl)[4][16], bool& ok, Clock& pc) {
   uint32_t X = 0, D = 0;
@@ -444,36 +444,36 @@ __device__ __forceinline__ void planes4(Lds& L, const Win& W, uint32_t w, uint32
     for (int v = 0; v < NWV; v++) all &= L.vok[v];
     ok = ok && all != 0;
   };
-#if TDBG_PLANE_BARRIERS == 1
-  uint32_t ae[4], be[4];
-  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae[0], be[0], pc);
-  plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae[1], be[1], pc);
-  plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae[2], be[2], pc);
-  plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae[3], be[3], pc);
-  sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
-  verdicts();
-  if (ok) {
-    plane_fold<0>(L, w, l, X, D, ae[0], be[0], xl[0]);
-    plane_fold<1>(L, w, l, X, D, ae[1], be[1], xl[1]);
-    plane_fold<2>(L, w, l, X, D, ae[2], be[2], xl[2]);
-    plane_fold<3>(L, w, l, X, D, ae[3], be[3], xl[3]);
+  if constexpr (PB == 1) {
+    uint32_t ae[4], be[4];
+    plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae[0], be[0], pc);
+    plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae[1], be[1], pc);
+    plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae[2], be[2], pc);
+    plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae[3], be[3], pc);
+    sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
+    verdicts();
+    if (ok) {
+      plane_fold<0>(L, w, l, X, D, ae[0], be[0], xl[0]);
+      plane_fold<1>(L, w, l, X, D, ae[1], be[1], xl[1]);
+      plane_fold<2>(L, w, l, X, D, ae[2], be[2], xl[2]);
+      plane_fold<3>(L, w, l, X, D, ae[3], be[3], xl[3]);
+    }
+  } else {
+    uint32_t ae = 0, be = 0;
+    plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae, be, pc);
+    sc::lds_barrier();
+    verdicts();
+    if (ok) plane_fold<0>(L, w, l, X, D, ae, be, xl[0]);
+    plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae, be, pc);
+    sc::lds_barrier();
+    if (ok) plane_fold<1>(L, w, l, X, D, ae, be, xl[1]);
+    plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae, be, pc);
+    sc::lds_barrier();
+    if (ok) plane_fold<2>(L, w, l, X, D, ae, be, xl[2]);
+    plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae, be, pc);
+    sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
+    if (ok) plane_fold<3>(L, w, l, X, D, ae, be, xl[3]);
   }
-#else
-  uint32_t ae = 0, be = 0;
-  plane<CB, 0, SGN>(L, W, w, l, x0, x1, xl[0], ae, be, pc);
-  sc::lds_barrier();
-  verdicts();
-  if (ok) plane_fold<0>(L, w, l, X, D, ae, be, xl[0]);
-  plane<CB, 1, SGN>(L, W, w, l, x0, x1, xl[1], ae, be, pc);
-  sc::lds_barrier();
-  if (ok) plane_fold<1>(L, w, l, X, D, ae, be, xl[1]);
-  plane<CB, 2, SGN>(L, W, w, l, x0, x1, xl[2], ae, be, pc);
-  sc::lds_barrier();
-  if (ok) plane_fold<2>(L, w, l, X, D, ae, be, xl[2]);
-  plane<CB, 3, SGN>(L, W, w, l, x0, x1, xl[3], ae, be, pc);
-  sc::lds_barrier();  // (also frees C and TAB for the next tile's DMA)
-  if (ok) plane_fold<3>(L, w, l, X, D, ae, be, xl[3]);
-#endif
 }
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
@@ -494,7 +494,7 @@ __device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, ui
   }
 }
 
-template <bool SGN, int STM>
+template <bool SGN, int STM, int PB>
 __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(const KParams kp) {
   __shared__ Lds L;
   const uint64_t G = gridDim.x;
@@ -654,7 +654,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     // plane's codes land directly in their value registers
     switch (ok ? cb : 0u) {
 #define TDBG_CB(c) \
-  case c: planes4<c, SGN>(L, W, w, l, x0, x1, xl, ok, pc); break;
+  case c: planes4<c, SGN, PB>(L, W, w, l, x0, x1, xl, ok, pc); break;
       TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
       TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
       TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
@@ -670,7 +670,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
 #pragma unroll
           for (int i = 0; i < 16; i++) xl[k][i] = 0;
 #pragma unroll
-        for (int k = 0; k < TDBG_PLANE_BARRIERS; k++) lds_barrier();
+        for (int k = 0; k < PB; k++) lds_barrier();
         break;
     }
     }  // cur_dma
@@ -772,12 +772,16 @@ extern "C" uint32_t tdbg_stream_grid(int cus) {
 // Launch: sgn = the BWR stage's integer type is signed.
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
   using namespace tdbg::stream;
-  // store mode: 1 nontemporal (default: 5 % faster than plain stores on C5
-  // active, profiles/r03_*), 0 plain, 3 no stores (timing ablation only)
+  // store mode: 1 nontemporal (5 % faster than plain stores on C5 active,
+  // profiles/r03_*), 3 no stores (timing ablation only, signed tiles)
   static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 1;
-  auto k = sgn ? (stm == 0 ? unfilter_stream_kernel<true, 0>
-                  : stm == 3 ? unfilter_stream_kernel<true, 3> : unfilter_stream_kernel<true, 1>)
-               : (stm == 0 ? unfilter_stream_kernel<false, 0> : unfilter_stream_kernel<false, 1>);
+  // one barrier per tile for short launches, one per plane for long ones
+  // (planes4); TDBG_STREAM_PB=1|4 forces one (experiments)
+  static const int pbe = getenv("TDBG_STREAM_PB") ? atoi(getenv("TDBG_STREAM_PB")) : 0;
+  const bool pb1 = pbe ? pbe == 1 : kp->ntiles < 48ull * grid;
+  auto k = stm == 3 ? unfilter_stream_kernel<true, 3, 4>
+           : sgn    ? (pb1 ? unfilter_stream_kernel<true, 1, 1> : unfilter_stream_kernel<true, 1, 4>)
+                    : (pb1 ? unfilter_stream_kernel<false, 1, 1> : unfilter_stream_kernel<false, 1, 4>);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
   return hipGetLastError();
 }
