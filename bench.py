@@ -317,8 +317,13 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
         if forward and vi == 0 and not ablation and cfgname != "fscale":  # (lossy: values differ)
             # (on at most one GPU's shard of C5, 12,500 tiles: the forward leg
             # checks every filtered tile against the encoder's bytes on the host)
-            res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx[: args.shard_tiles or ntiles], pool, steps,
-                                           warmup, dist)
+            try:
+                res[var]["fwd"] = time_forward(engine, ctx, dp, vals, idx[: args.shard_tiles or ntiles], pool, steps,
+                                               warmup, dist)
+            except SystemExit as ex:
+                if cfgname == args.config:
+                    raise
+                res[var]["fwd_error"] = str(ex)  # (other configs' legs: reported, not fatal)
         if e2e_leg:
             ne = min(ntiles, args.e2e_tiles) if args.e2e_tiles else ntiles
             res[var]["e2e"] = e2e(engine, ctx, dp, packed, offs[:ne], sizes[:ne], int(vals[0].nbytes), args, dist,
@@ -467,6 +472,40 @@ def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, 
 OTHER_CONFIGS = ("c1", "c2", "c2i", "c3a", "c3b", "c4")
 
 
+FORWARD_KERNEL = {
+    "c5": "filter_stream_c5_kernel (tdbg_forward_stream.hip) + filter_tiles_kernel on its queue",
+    "c3a": "filter_small_kernel<0> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
+    "c3b": "filter_small_kernel<1> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
+    "c4": "filter_small_kernel<2> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
+    "c1": "filter_shuffle4_kernel<0> (tdbg_forward_shuffle.hip) + filter_tiles_kernel on its queue",
+    "c2": "filter_shuffle4_kernel<1> (tdbg_forward_shuffle.hip) + filter_tiles_kernel on its queue",
+    "c2i": "filter_shuffle4_kernel<2> (tdbg_forward_shuffle.hip) + filter_tiles_kernel on its queue",
+}
+
+
+def forward_line(cfgname, variants, res, world):
+    """The forward (filter) leg of a config's first variant, if it ran."""
+    fv = variants[0]
+    if "fwd_error" in res[fv]:
+        return {"variant": fv, "error": res[fv]["fwd_error"]}
+    if "fwd" not in res[fv]:
+        return None
+    r = res[fv]
+    el, fk, fb_alg, fin = r["fwd"]
+    return {
+        "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
+        "variant": fv,
+        "tiles_per_gpu": int(round(fin / r["out_bytes"])),
+        "value": round(fin * world / (el / r["steps"]) / 2**30, 2),
+        "unit": "GiB/s",
+        "ms_per_step": round(el / r["steps"] * 1e3, 4),
+        "kernel": FORWARD_KERNEL.get(cfgname, "filter_tiles_kernel (general forward kernel)"),
+        "kernel_ms": round(fk, 4),
+        "algorithmic_bytes_per_launch": int(fb_alg),
+        "roofline_frac": round(fb_alg / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+
+
 def headline_line(args, W, variants, res, world):
     """The JSON line of the bench's config: `value` is the slowest variant
     (SURVEY 8(d) defines C5's 'ramp' and 'rand'; 'active' makes all three
@@ -506,21 +545,9 @@ def headline_line(args, W, variants, res, world):
     line["config"]["variants"] = {v: variant_line(args.config, v, res[v], world) for v in variants}
     line["config"]["min_over_variants_GiBps"] = round(min(gibps(res[v], world) for v in variants), 2)
     line["config"]["min_over_variants_roofline_frac"] = round(min(frac(res[v]) for v in variants), 4)
-    fv = variants[0]
-    if "fwd" in res[fv]:
-        el, fk, fb_alg, fin = res[fv]["fwd"]
-        line["forward"] = {
-            "metric": "GiB/s unfiltered tile bytes filtered (device-resident), same tiles and pipeline",
-            "variant": fv,
-            "tiles_per_gpu": int(round(fin / r["out_bytes"])),
-            "value": round(fin * world / (el / r["steps"]) / 2**30, 2),
-            "unit": "GiB/s",
-            "ms_per_step": round(el / r["steps"] * 1e3, 4),
-            "kernel": "filter_tiles_kernel",
-            "kernel_ms": round(fk, 4),
-            "algorithmic_bytes_per_launch": int(fb_alg),
-            "roofline_frac": round(fb_alg / (fk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        }
+    fl = forward_line(args.config, variants, res, world)
+    if fl:
+        line["forward"] = fl
     if all("e2e" in res[v] for v in variants):
         line["config"]["e2e_GiBps"] = {v: res[v]["e2e"] for v in variants}
         line["config"]["e2e_note"] = ("pinned host tiles -> H2D -> unfilter -> D2H into a pinned result buffer, "
@@ -622,12 +649,15 @@ def main():
             cc = CONFIGS[c]
             cvars = [v for v in cc["variants"].split(",") if v]
             cdp, cres = run_config(engine, ctx, W, args, c, cvars, cc["tiles_per_gpu"], args.steps, args.warmup,
-                                   dist, world, rank)
+                                   dist, world, rank, forward=args.forward)
             ch = min(cvars, key=lambda v: gibps(cres[v], world))
             o = {"workload": cc["workload"], "tiles_per_gpu": cc["tiles_per_gpu"], "dtype": cc["dtype"],
                  "value_GiBps": round(gibps(cres[ch], world), 2), "variant": ch,
                  "roofline": roofline(c, ch, cres[ch]),
                  "variants": {v: variant_line(c, v, cres[v], world) for v in cvars}}
+            fl = forward_line(c, cvars, cres, world)
+            if fl:
+                o["forward"] = fl
             if not args.no_cpu_baseline:
                 o["cpu_baseline"] = cpu_line(engine, cdp, cres[ch], c, ch, threads, args.cpu_seconds_other)
             if c == "c1":

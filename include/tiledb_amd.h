@@ -335,10 +335,12 @@ int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles);
  * as the one-chunk tiles are).  Cumulative; waits for the context's last
  * launch. */
 int tdbg_context_stream_chunk_stats(const tdbg_context* c, uint64_t* chunks);
-/* Forward direction: tiles the LDS-resident kernel for [BYTESHUFFLE,
- * DOUBLE_DELTA, BWR(256)] on INT32 / UINT32 64 KiB tiles filtered
- * (tdbg_forward_stream.hip; the others run on the general forward kernel).
- * Cumulative; waits for the context's last launch. */
+/* Forward direction: tiles the LDS-resident forward kernels filtered --
+ * [BYTESHUFFLE, DOUBLE_DELTA, BWR(256)] on INT32 / UINT32
+ * (tdbg_forward_stream.hip) and, on 8-byte values, [DOUBLE_DELTA], [RLE] and
+ * [POSITIVE_DELTA(1024), BWR(256)] (tdbg_forward_small.hip), 64 KiB tiles;
+ * the others run on the general forward kernel.  Cumulative; waits for the
+ * context's last launch. */
 int tdbg_context_forward_stream_stats(const tdbg_context* c, uint64_t* tiles);
 
 /* Device-side time (ms) of the last *armed* tdbg_unfilter_tiles_* launch on

@@ -586,7 +586,13 @@ def test_chunk_stream_multichunk(eng, ctx, oracle_mod, variant):
     f1, b1, _ = ctx.path_stats()
     assert not st.any()
     assert b1 - b0 == 0 and f1 - f0 == n
-    assert ctx.stream_chunks() - c0 == 15 * n  # every full chunk; the short last ones went to the fused kernel
+    # every full chunk of a tile whose output starts 16-B aligned (the
+    # streaming kernels' store rule; the outputs here are packed back to
+    # back, and these tiles' sizes are 4 mod 16 apart); the short last ones
+    # and the unaligned tiles' chunks went to the fused kernel
+    aligned = sum(int(batch.out_off[i]) % 16 == 0 for i in range(n))
+    assert 0 < aligned < n
+    assert ctx.stream_chunks() - c0 == 15 * aligned
     out = batch.outputs_host()
     for i in range(n):
         o = int(batch.out_off[i])

@@ -23,6 +23,8 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
           ("tdbg_forward_stream.hip", "tdbg_forward_stream", []),
+          ("tdbg_forward_small.hip", "tdbg_forward_small", []),
+          ("tdbg_forward_shuffle.hip", "tdbg_forward_shuffle", []),
           ("tdbg_stream_shuffle.hip", "tdbg_stream_shuffle", []),
           ("tdbg_dense.hip", "tdbg_dense", []),
           ("tdbg_io.cpp", "tdbg_io", []),

@@ -312,11 +312,22 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       }
       uint64_t mx = (uint64_t)mxd;
       mx = row_max64(mx);
-      if ((l & 15) == 0) L.red[4 * w + (l >> 4)] = mx;
+      // the wave's maximum from its four rows (readlane: scalar), one LDS
+      // entry per wave
+      {
+        auto rl = [&](int k) -> uint64_t {
+          return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(mx >> 32), k) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((uint32_t)mx, k);
+        };
+        const uint64_t a = rl(0), b = rl(16), c = rl(32), d = rl(48);
+        const uint64_t ab = a > b ? a : b, cd = c > d ? c : d;
+        mx = ab > cd ? ab : cd;
+      }
+      if (l == 0) L.red[w] = mx;
       __syncthreads();  // B1
       mx = 0;
 #pragma unroll
-      for (int v = 0; v < 4 * NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
+      for (int v = 0; v < NWV; v++) mx = L.red[v] > mx ? L.red[v] : mx;
       // (the 64-bit extensions of the bit-size pass are recomputed below, not
       // kept live across the barrier: 40 values would take 80 registers)
 #pragma unroll

@@ -29,6 +29,10 @@ extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
 extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
 extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
+extern "C" hipError_t tdbg_launch_filter_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
+                                               hipStream_t s);
+extern "C" hipError_t tdbg_launch_filter_shuffle4(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
+                                                  hipStream_t s);
 extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
                                             tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
                                             uint64_t* need, hipStream_t stream);
@@ -1063,7 +1067,61 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
                   P.s[1].w == 4 && P.s[2].w == 4 && P.s[2].dts == 4 && P.s[1].sgn == P.s[2].sgn &&
                   P.s[2].window == 256 && p->cell_size == 4 && (max_chunk == 0 || max_chunk >= 65536) &&
                   n <= c->status_cap;
+  // The scan configs' pipelines on 8-byte values -- C3a [DOUBLE_DELTA]
+  // (mode 0), C3b [RLE] with 8-byte cells (mode 1), C4 [POSITIVE_DELTA(1024),
+  // BWR(256)] on uint64 (mode 2) -- with one
+  // 64 KiB chunk per tile go through the LDS-resident small forward kernel
+  // (tdbg_forward_small.hip) first, the same way
+  const int fsmall = (no_fast || d_list || c5 || p->cell_size != 8 || (max_chunk != 0 && max_chunk < 65536) ||
+                      n > c->status_cap)
+                         ? -1
+                     : (P.fast == 12 && P.nstages == 1 && P.s[0].w == 8)  ? 0
+                     : (P.fast == 14 && P.nstages == 1 && P.s[0].cs == 8) ? 1
+                     : ((P.fast == 15 || P.fast == 16) && P.nstages == 2 && P.s[0].kind == TDBG_K_PD &&
+                        P.s[1].kind == TDBG_K_BWR && P.s[0].w == 8 && P.s[0].dts == 8 && P.s[1].w == 8 &&
+                        P.s[1].dts == 8 && !P.s[0].sgn && !P.s[1].sgn && P.s[0].window == 1024 &&
+                        P.s[1].window == 256)
+                         ? 2
+                         : -1;
+  // C1 [BYTESHUFFLE] (mode 0), C2 [BITSHUFFLE] + pass-through BWR (mode 1)
+  // and C2i [BITSHUFFLE, BWR(256)] (mode 2) on 4-byte values: the shuffle
+  // forward kernel (tdbg_forward_shuffle.hip), the same way
+  const bool sh_ok = !no_fast && !d_list && !c5 && p->cell_size == 4 && (max_chunk == 0 || max_chunk >= 65536) &&
+                     n <= c->status_cap && P.s[0].w == 4;
+  const int fshuf = !sh_ok ? -1
+                    : (P.nstages == 1 && P.s[0].kind == TDBG_K_BYTESHUFFLE) ? 0
+                    : (P.s[0].kind == TDBG_K_BITSHUFFLE &&
+                       (P.nstages == 1 || (P.nstages == 2 && P.s[1].kind == TDBG_K_PASS)))
+                        ? 1
+                    : (P.nstages == 2 && P.s[0].kind == TDBG_K_BITSHUFFLE && P.s[1].kind == TDBG_K_BWR &&
+                       P.s[1].w == 4 && P.s[1].dts == 4 && P.s[1].window == 256)
+                        ? 2
+                        : -1;
   hipError_t e = hipSuccess;
+  if (fshuf >= 0) {
+    HIP_OK(hipMemsetAsync(c->d_fbq, 0, sizeof(uint32_t), s));
+    tdbg::KParams kf = kp;
+    kf.fbq = c->d_fbq;
+    kf.fbq_cap = (uint32_t)n;
+    kf.stats = c->d_stats;
+    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
+    e = tdbg_launch_filter_shuffle4(&kf, fgrid, fshuf, fshuf == 2 && P.s[1].sgn ? 1 : 0, s);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward shuffle launch: ") + hipGetErrorString(e));
+    kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
+    kp.ntiles_dev = c->d_fbq;
+  }
+  if (fsmall >= 0) {
+    HIP_OK(hipMemsetAsync(c->d_fbq, 0, sizeof(uint32_t), s));
+    tdbg::KParams kf = kp;
+    kf.fbq = c->d_fbq;
+    kf.fbq_cap = (uint32_t)n;
+    kf.stats = c->d_stats;
+    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * (fsmall == 2 ? 3 : 4));
+    e = tdbg_launch_filter_small(&kf, fgrid, fsmall, fsmall == 0 && P.s[0].sgn ? 1 : 0, s);
+    if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward small launch: ") + hipGetErrorString(e));
+    kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
+    kp.ntiles_dev = c->d_fbq;
+  }
   if (c5) {
     HIP_OK(hipMemsetAsync(c->d_fbq, 0, sizeof(uint32_t), s));
     tdbg::KParams kf = kp;

@@ -26,8 +26,10 @@
 //     fit the 8 KB staging); the affine double-delta aggregate of its
 //     codes goes through a DPP wave scan and one LDS exchange per round.
 //   * RLE⁻¹ (rle_compressor.cc:103-141): one workgroup scan of the run
-//     lengths gives the run starts; each lane finds the run of its first cell
-//     by a branch-free binary search and walks forward.
+//     lengths gives the run starts; every run writes its index at each
+//     16-cell group start it holds (a run-head scatter: 512 writes per tile),
+//     so a lane finds the run of its first cell with one LDS read and walks
+//     forward.
 //   * BWR⁻¹ then PD⁻¹ (bit_width_reduction_filter.cc:352-404,
 //     positive_delta_filter.cc:324-375): one pass over the window headers
 //     builds both window tables; a lane's 16 values lie in one BWR window
@@ -82,6 +84,7 @@ struct Tab<M_DD> {
 template <>
 struct Tab<M_RLE> {
   uint32_t RS[RUNCAP + 4];  // run starts in cells; RS[r] = total for r >= nr
+  uint16_t HD[NV / 16];     // the run holding cell 16 g
   uint32_t wt[NWV];
 };
 template <>
@@ -435,6 +438,11 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           L.T.RS[4 * threadIdx.x + i] = a;
+          // run-head scatter: the run holding cell 16 g, for every 16-cell
+          // group start inside this run (each written once: the runs tile
+          // [0, 8192) when tot == NV; empty runs hold none)
+          if (ok)
+            for (uint32_t g = (a + 15) >> 4; 16 * g < a + len[i]; g++) L.T.HD[g] = (uint16_t)(4 * threadIdx.x + i);
           a += len[i];
         }
         if (threadIdx.x == NT - 1) L.T.RS[RUNCAP] = a;
@@ -544,13 +552,9 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
         } else if constexpr (MODE == M_RLE) {
           if (ok) {
             const uint32_t c0 = 4096 * h + 1024 * w + 16 * l;
-            // the last run start <= c0 (RS[nr] = 8192 > c0; empty runs skipped)
-            uint32_t r = 0;
-#pragma unroll
-            for (uint32_t st = RUNCAP / 2; st >= 1; st >>= 1) {
-              const uint32_t q = r + st;
-              r = (q <= hd.nr && L.T.RS[q] <= c0) ? q : r;
-            }
+            // the run holding c0 (a multiple of 16): one read of the
+            // run-head scatter instead of a dependent binary search
+            uint32_t r = L.T.HD[c0 >> 4];
             uint32_t rend = L.T.RS[r + 1];
             uint64_t x = c64(L.C, hd.dst + 10 * r);
 #pragma unroll
