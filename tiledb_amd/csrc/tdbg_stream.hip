@@ -515,20 +515,45 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
   Desc cur{};
   bool cur_dma = false;
   bool stored = false;  // the last iteration issued its 16 output stores after the DMA
+  // The workgroup's k-th tile is blockIdx.x + k G; descriptors come 64 at a
+  // time (bt, batch base bbase).  This kernel owns the tiles of at most
+  // CCAP bytes (it decodes them or queues them); the bigger ones belong to
+  // the raw-DoubleDelta kernel and are skipped a batch at a time (mine: the
+  // batch's owned tiles), so a launch of raw tiles costs this kernel two
+  // descriptor loads per workgroup, not a walk over every tile.
   Batch bt{0, 0, 0, 0};
-  if (blockIdx.x < ntl) {
-    bt = batch_load(kp, 0, ntl);
-    cur = batch_get(bt, 0, blockIdx.x);
+  uint64_t bbase = ~0ull, mine = 0;
+  // smallest owned tile index >= from (false: none left)
+  auto next_owned = [&](uint64_t from, uint64_t& nit) -> bool {
+    for (;;) {
+      const uint64_t base = from - from % 64;
+      if (blockIdx.x + base * G >= ntl) return false;
+      if (base != bbase) {
+        bt = batch_load(kp, base, ntl);
+        const uint64_t jl = blockIdx.x + (base + lane_()) * G;
+        mine = __builtin_amdgcn_ballot_w64(jl < ntl && bt.fs <= CCAP);
+        bbase = base;
+      }
+      const uint64_t m = mine & (~0ull << (from - base));
+      if (m) {
+        nit = base + (uint64_t)__builtin_ctzll(m);
+        return true;
+      }
+      from = base + 64;
+    }
+  };
+  uint64_t it = 0;
+  bool have = next_owned(0, it);
+  if (have) {
+    cur = batch_get(bt, (uint32_t)(it % 64), blockIdx.x + it * G);
     cur_dma = fits(cur);
     if (cur_dma) dma(L, cur);
   }
-  // tiles left to the fused kernel, this batch: bit i = iteration i % 64
+  // tiles left to the fused kernel, this batch: bit i = batch position i
   // (queued with one atomic per workgroup and batch: a single global counter
   // taking one atomic per tile serialises the whole grid on it)
   uint64_t dmask = 0;
-  uint32_t it = 0;
-  for (uint64_t j = blockIdx.x; j < ntl; j += G, it++) {
-    const uint64_t jn = j + G;
+  while (have) {
     const uint32_t l = lane_();
     // A tile whose image does not fit is declined without touching LDS (and
     // without barriers: no wave reads C for it, and the last tile that did
@@ -677,14 +702,20 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     // tiles bigger than CCAP belong to the raw-DoubleDelta kernel, which runs
     // next on every tile and queues the ones it does not take itself
     if (!ok && cur.fs <= CCAP) dmask |= 1ull << (it % 64);
-    if ((it + 1) % 64 == 0 || jn >= ntl) {
-      if (dmask && w == 0) queue_batch(kp, dmask, it - it % 64);
+    const uint64_t cbase = it - it % 64;
+    uint64_t nit = 0;
+    const bool hn = next_owned(it + 1, nit);  // (may load later batches: before the DMA)
+    if (!hn || nit - nit % 64 != cbase) {
+      if (dmask && w == 0) queue_batch(kp, dmask, (uint32_t)cbase);
       dmask = 0;
     }
-    if ((it + 1) % 64 == 0 && jn < ntl) bt = batch_load(kp, it + 1, ntl);
-    const Desc nxt = batch_get(bt, (it + 1) % 64, jn);
-    const bool nxt_dma = jn < ntl && fits(nxt);
-    if (nxt_dma) dma(L, nxt);
+    Desc nxt{};
+    bool nxt_dma = false;
+    if (hn) {
+      nxt = batch_get(bt, (uint32_t)(nit % 64), blockIdx.x + nit * G);
+      nxt_dma = fits(nxt);
+      if (nxt_dma) dma(L, nxt);
+    }
     if (ok) {
       pc.mark(14);
       // byteshuffle⁻¹: unit i of the lane = dword i of the four planes,
@@ -745,6 +776,8 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
     cur = nxt;
     cur_dma = nxt_dma;
     stored = ok;
+    it = nit;
+    have = hn;
     pc.mark(15);
   }
   pc.flush();
