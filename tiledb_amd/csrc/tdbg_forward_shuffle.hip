@@ -19,8 +19,8 @@
 // 4x4 transposes assemble, per row, the dword of the lane's four groups --
 // so row r of block b is exactly the wave's 64 dwords, written by one store
 // instruction (256 consecutive bytes).  That row is also BWR window
-// 32 b + r (256-B windows over the shuffled part): C2i reduces it across
-// the wave (min / max -> width), the 256 window sizes go through one
+// 32 b + r (256-B windows over the shuffled part): C2i reduces it through
+// the wave's LDS area (min / max -> width), the 256 window sizes go through one
 // workgroup scan, and each window is written compressed where the scan put
 // it (8-bit: a quad's four bytes as one dword, 16-bit: a pair's halves).
 // Byteshuffle (C1): the lane's 32 elements give, per plane, 32 bytes of
@@ -135,6 +135,7 @@ __device__ __forceinline__ void st8(uint8_t* base, uint32_t off, uint32_t v) { b
 template <int MODE, bool SGN>
 __global__ void __launch_bounds__(NT, 2) filter_shuffle4_kernel(const KParams kp) {
   __shared__ uint32_t wsz[NWV];  // C2i: compressed bytes of each wave's 32 windows
+  __shared__ uint32_t red[MODE == 2 ? NWV : 1][8][64];  // C2i: a wave's 8 rows being reduced
   uint64_t taken = 0;
   for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
     uint32_t T = threadIdx.x;
@@ -212,19 +213,54 @@ __global__ void __launch_bounds__(NT, 2) filter_shuffle4_kernel(const KParams kp
             for (int r = 0; r < 32; r++) st32(o, 256 * r, R[r]);
           }
         } else {
-          // ---- C2i: BWR window 32 w + r = row r of this wave's block ----
-          uint32_t bitsv = 0, minv = 0;  // lane r < 32: window r's width and offset
+          // ---- C2i: BWR window 32 w + r = row r of this wave's block.  Its
+          // min / max: the wave's rows go through its LDS area 8 at a time
+          // (lane l then reduces 8 dwords of row l / 8, and 3 DPP steps
+          // finish the row in its 8 lanes) instead of 32 full-wave DPP
+          // reductions; round q's lane 8 i holds row 8 q + i's width and
+          // offset ----
+          uint32_t rb[4], rm[4];
           uint32_t wtot = 0;
 #pragma unroll
-          for (int r = 0; r < 32; r++) {
-            uint32_t mn, mx, mv;
-            wave_minmax32<SGN>(R[r], mn, mx);
-            const uint32_t bits = window_bits<SGN>(mn, mx, mv);
-            if (l == (uint32_t)r) {
-              bitsv = bits;
-              minv = mv;
+          for (int q = 0; q < 4; q++) {
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; i++) red[w][i][l] = R[8 * q + i];
+            __builtin_amdgcn_wave_barrier();  // (one wave: its LDS operations complete in order)
+            const uint32_t row = l >> 3, seg = l & 7;
+            const v4u a = *(const v4u*)&red[w][row][8 * seg], b = *(const v4u*)&red[w][row][8 * seg + 4];
+            const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint32_t mn = x[0], mx = x[0];
+#pragma unroll
+            for (int i = 1; i < 8; i++) {
+              if (SGN) {
+                mn = (int32_t)x[i] < (int32_t)mn ? x[i] : mn;
+                mx = (int32_t)x[i] > (int32_t)mx ? x[i] : mx;
+              } else {
+                mn = x[i] < mn ? x[i] : mn;
+                mx = x[i] > mx ? x[i] : mx;
+              }
             }
-            wtot += bits == 8 ? 64u : bits == 16 ? 128u : 256u;
+            auto comb = [&](uint32_t m2, uint32_t x2) {
+              if (SGN) {
+                mn = (int32_t)m2 < (int32_t)mn ? m2 : mn;
+                mx = (int32_t)x2 > (int32_t)mx ? x2 : mx;
+              } else {
+                mn = m2 < mn ? m2 : mn;
+                mx = x2 > mx ? x2 : mx;
+              }
+            };
+            comb(dpp_<0xB1>(mn), dpp_<0xB1>(mx));    // lanes i ^ 1
+            comb(dpp_<0x4E>(mn), dpp_<0x4E>(mx));    // lanes i ^ 2
+            comb(dpp_<0x141>(mn), dpp_<0x141>(mx));  // row half mirror: lanes 7 - i of the 8
+            uint32_t mv;
+            rb[q] = window_bits<SGN>(mn, mx, mv);
+            rm[q] = mv;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+              const uint32_t bits = __builtin_amdgcn_readlane(rb[q], 8 * i);
+              wtot += bits == 8 ? 64u : bits == 16 ? 128u : 256u;
+            }
           }
           if (l == 0) wsz[w] = wtot;
           __syncthreads();  // B1: every wave's total
@@ -249,22 +285,25 @@ __global__ void __launch_bounds__(NT, 2) filter_shuffle4_kernel(const KParams kp
               st32(out, 20 + ML_BWR, 1);  // bitshuffle md: one part of 65,536 B
               st32(out, 24 + ML_BWR, TB);
             }
-            if (l < 32) {  // window 32 w + l's md entry [i32 min][u8 bits][u32 256] (9 B)
-              const uint32_t eo = 28 + 9 * (32 * w + l);
+            if ((l & 7) == 0) {  // windows 32 w + 8 q + l / 8: md entries [i32 min][u8 bits][u32 256] (9 B)
 #pragma unroll
-              for (int i = 0; i < 4; i++) st8(out, eo + i, minv >> (8 * i));
-              st8(out, eo + 4, bitsv);
-              st8(out, eo + 5, 0);
-              st8(out, eo + 6, 1);
-              st8(out, eo + 7, 0);
-              st8(out, eo + 8, 0);
+              for (int q = 0; q < 4; q++) {
+                const uint32_t eo = 28 + 9 * (32 * w + 8 * q + (l >> 3));
+#pragma unroll
+                for (int i = 0; i < 4; i++) st8(out, eo + i, rm[q] >> (8 * i));
+                st8(out, eo + 4, rb[q]);
+                st8(out, eo + 5, 0);
+                st8(out, eo + 6, 1);
+                st8(out, eo + 7, 0);
+                st8(out, eo + 8, 0);
+              }
             }
             // the windows' data, in order (offsets: multiples of 4)
             uint32_t off = D0_C2I + pre;
 #pragma unroll
             for (int r = 0; r < 32; r++) {
-              const uint32_t bits = __builtin_amdgcn_readlane(bitsv, r);
-              const uint32_t rel = R[r] - __builtin_amdgcn_readlane(minv, r);
+              const uint32_t bits = __builtin_amdgcn_readlane(rb[r >> 3], 8 * (r & 7));
+              const uint32_t rel = R[r] - __builtin_amdgcn_readlane(rm[r >> 3], 8 * (r & 7));
               if (bits == 32) {
                 st32(out, off + 4 * l, R[r]);
                 off += 256;
