@@ -249,6 +249,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
 #pragma unroll
     for (int i = 0; i < 10; i++) U[i] = src[(8 * T + i - 2) & 4095u];
   };
+  bool pre = false;  // U holds this tile's units already (loaded at the end of the last iteration)
   for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
     // thread index opaque to the optimizer: the unrolled per-thread index
     // math is tile-invariant, and hoisting it out of the tile loop pins (and
@@ -264,10 +265,11 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
     bool ok = shape;
     __syncthreads();  // B0: the last tile's image is stored (LDS free)
     if (shape) {
-      // (issued first: their latency overlaps the zeroing below; a prefetch
-      // one tile ahead, issued before the last tile's image store, measured
-      // slower: the store phase waited behind the loads)
-      load_units(t, T);
+      // (issued here, their latency overlaps the zeroing below, unless the
+      // last iteration already issued them right after its image stores:
+      // then they also overlap B0.  A prefetch issued before the last tile's
+      // image stores measured slower -- the stores waited behind the loads.)
+      if (!pre) load_units(t, T);
       // ---- zero the DD word region (codes are OR-ed in) ----
       static_assert(BDW % 4 == 0, "16-B zeroing");
       for (uint32_t d = (WD0 & ~3u) + 4 * T; d < BDW; d += 4 * NT) *(v4u*)(L.B + d) = v4u{0u, 0u, 0u, 0u};
@@ -565,6 +567,14 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           if (kp.out_len) kp.out_len[t] = total;
         }
       }
+    }
+    // the next tile's units, behind this tile's stores
+    pre = false;
+    if (j + gridDim.x < kp.ntiles && shape_of(j + gridDim.x)) {
+      uint32_t Tn = threadIdx.x;
+      asm volatile("" : "+v"(Tn));
+      load_units(j + gridDim.x, Tn);
+      pre = true;
     }
     pc.mark(6);
     if (!ok && T == 0) {
