@@ -1146,7 +1146,11 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
     kp.ntiles_dev = c->d_fbq;
   }
-  e = tdbg_launch_filter(&kp, grid, s);
+  // On a fast kernel's queue the general kernel sees only the tiles that
+  // kernel declined (unusual shapes): a small grid, since dispatching the
+  // full one costs ~28 us even when the queue is empty (C1 forward trace,
+  // profiles/r04/c1_forward_trace_kernel_stats.csv)
+  e = tdbg_launch_filter(&kp, kp.ntiles_dev ? std::min<uint32_t>(grid, 64) : grid, s);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("filter launch: ") + hipGetErrorString(e));
   return TDBG_OK;
 }
