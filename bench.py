@@ -26,6 +26,7 @@ import json
 import os
 import sys
 import time
+import zlib
 
 import numpy as np
 
@@ -296,7 +297,8 @@ def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, d
     res = {}
     for vi, var in enumerate(variants):
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
-            engine, cfgname, var, ntiles, args.unique, torch.cuda.current_device(), seed=5 + 1000 * rank + vi,
+            engine, cfgname, var, ntiles, args.unique, torch.cuda.current_device(),
+            seed=5 + 1000 * rank + zlib.crc32(var.encode()) % 997,  # (by name: a --variants run sees the same tiles)
             align=align, ctx=ctx, dp=dp)
         st = ctx.unfilter(dp, batch)  # synchronous first pass (status + retry path)
         if st.any():
