@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 cd $R
 A="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
 C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"
-B="--config c5 --variants active --no-cpu-baseline --no-e2e --no-others --steps 5 --warmup 2"
+B="--config c5 --variants active --tiles-per-gpu 12500 --no-cpu-baseline --no-e2e --no-others --steps 5 --warmup 2"
 P=0
 for SET in "$A" "$C"; do
   P=$((P+1))
