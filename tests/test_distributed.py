@@ -75,7 +75,7 @@ def _worker(rank: int, world: int, port: int, q):
         packed = np.concatenate(bufs)
         offs = np.concatenate([[0], np.cumsum(isz[lo:hi])[:-1]]).astype(np.uint64)
         elapsed = bench.max_over_ranks(dist, el, "cpu")
-        r = dict(elapsed=elapsed, kern_ms=el * 1e3, launch_ms=el * 1e3, b_alg=float(isz[lo:hi].sum() + osz[lo:hi].sum()),
+        r = dict(elapsed=elapsed, ev_elapsed=elapsed, kern_ms=el * 1e3, launch_ms=el * 1e3, b_alg=float(isz[lo:hi].sum() + osz[lo:hi].sum()),
                  unf=float(osz[lo:hi].sum()), unf_job=bench.sum_over_ranks(dist, float(osz[lo:hi].sum()), "cpu"),
                  out_bytes=W.TILE_BYTES, fused=hi - lo, fallback=0, streamed=hi - lo,
                  packed=packed, offs=offs, sizes=isz[lo:hi], steps=1, ntiles=hi - lo)

@@ -396,21 +396,30 @@ def test_host_end_to_end_padded_layouts(eng, ctx, oracle_mod):
     assert (res[mask] == 0xAB).all()
 
 
-def test_async_api_and_timing(eng, ctx, oracle_mod):
+@pytest.mark.parametrize("case", _CONFIG, ids=lambda c: c.name)
+def test_async_api_and_timing(eng, ctx, oracle_mod, case):
+    """Armed launches time their kernels with events bound to the dispatches
+    (tdbg_launch.h): per launch, kernel time > 0 and launch time >= it, on the
+    streamed (C1, C3-C5), fused-only (C2) and chunk-parallel paths alike."""
     import torch
-    case = _CONFIG[0]
     _, enc = encode(oracle_mod, case)
     dp = eng.DevicePipeline(case.serialized, case.version, int(case.dtype), case.cell_size)
     batch = eng.TileBatch.from_host([e[0] for e in enc], [e[2] for e in enc])
-    ctx.time_launches(1)  # events only on armed launches
+    ctx.time_launches(2)  # events only on armed launches
     ctx.unfilter_async(dp, batch)
+    ctx.unfilter_async(dp, batch, chunk_parallel=True)
     torch.cuda.synchronize()
     assert not batch.d_status.cpu().numpy().any()
     assert ctx.last_kernel_ms() > 0
+    kern, total = ctx.launch_times()
+    assert len(kern) == 2 and (kern > 0).all() and (total >= kern).all(), (kern, total)
     out = batch.outputs_host()
     for i, e in enumerate(enc):
         o = int(batch.out_off[i])
         assert np.array_equal(out[o:o + e[1].size], e[1])
+    ctx.unfilter_async(dp, batch)  # unarmed: no events
+    torch.cuda.synchronize()
+    assert len(ctx.launch_times()[0]) == 0  # reading the times disarmed the context
 
 
 def test_filter_pipeline_run_reverse_api(eng, oracle_mod):

@@ -35,7 +35,7 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           for k in range(NPART)])
 HOST_ONLY = {"tdbg_cpu.cpp"}
 NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip"}  # checked with -Rpass-analysis
-HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h"]
+HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h", "tdbg_launch.h"]
 
 
 def _deps(src: str):

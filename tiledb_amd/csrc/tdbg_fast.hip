@@ -19,6 +19,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 #include "tdbg_device.h"
 
 #include <type_traits>
@@ -2475,7 +2476,7 @@ namespace {
 template <int ID, int A, int B, int C, int D>
 hipError_t launch_spec(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream) {
   if constexpr (ID % TDBG_NPART == TDBG_PART) {
-    hipLaunchKernelGGL((tdbg::unfilter_fused_kernel<A, B, C, D>), dim3(grid), dim3(tdbg::FNT), 0, stream,
+    TDBG_LAUNCH((tdbg::unfilter_fused_kernel<A, B, C, D>), dim3(grid), dim3(tdbg::FNT), stream,
                        *kp);
     return hipGetLastError();
   } else {

@@ -22,6 +22,11 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
+
+namespace tdbg {
+thread_local EvArm ev_arm{nullptr, nullptr};  // tdbg_launch.h
+}
 
 extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
                                           hipStream_t stream);
@@ -764,9 +769,22 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // loop over chunks, filter_pipeline.cc:439-517)
   const bool chunk_stream = chunked && (c5_stream || small_mode >= 0) && !no_stream && !d_list && c->d_cq != nullptr;
   hipEvent_t* te = c->tcount < c->tcap ? &c->tev[3 * c->tcount++] : nullptr;
-  // Events only on armed launches (tdbg_context_time_launches): an event
-  // record costs ~3 % of a 12,500-tile C5 launch on the stream's timeline.
-  if (te) HIP_OK(hipEventRecord(te[0], stream));
+  // Events only on armed launches (tdbg_context_time_launches), and bound to
+  // the kernel dispatches themselves (tdbg_launch.h): te[0] = start of the
+  // first kernel, te[1] = end of the fused/general kernel, te[2] = end of the
+  // fixup.  Recorded as marker packets they cost ~4 us of stream time each.
+  struct Disarm {  // no armed event outlives this launch (error returns included)
+    ~Disarm() { tdbg::ev_arm = tdbg::EvArm{nullptr, nullptr}; }
+  } disarm;
+  // an armed event no dispatch took (ablations, no fixup): a marker packet
+  auto settle = [&]() -> hipError_t {
+    hipError_t r = hipSuccess;
+    if (tdbg::ev_arm.start) r = hipEventRecord(tdbg::ev_arm.start, stream);
+    if (r == hipSuccess && tdbg::ev_arm.stop) r = hipEventRecord(tdbg::ev_arm.stop, stream);
+    tdbg::ev_arm = tdbg::EvArm{nullptr, nullptr};
+    return r;
+  };
+  if (te) tdbg::ev_arm.start = te[0];
   hipError_t e = hipSuccess;
   static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
   static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
@@ -794,8 +812,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kf.ntiles = cap;
     kf.tile_list = c->d_cq + 1;
     kf.ntiles_dev = c->d_cq;
+    if (te) tdbg::ev_arm.stop = te[1];
     if (!skip_fused) e = tdbg_launch_fast(&kf, grid, stream);
-    if (te) HIP_OK(hipEventRecord(te[1], stream));
   } else if (streamed) {
     tdbg::KParams ks = kp;
     ks.sq = c->d_sq;
@@ -820,13 +838,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
     kf.tile_list = c->d_sq + 1;
     kf.ntiles_dev = c->d_sq;
+    if (te) tdbg::ev_arm.stop = te[1];  // kernel time = the streaming kernels + the fused one
     if (!skip_fused) e = tdbg_launch_fast(&kf, grid, stream);
-    if (te) HIP_OK(hipEventRecord(te[1], stream));  // kernel time = both kernels
   } else {
+    if (te) tdbg::ev_arm.stop = te[1];
     if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
-    if (te) HIP_OK(hipEventRecord(te[1], stream));
   }
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e));
+  if (te) HIP_OK(settle());
   if (queued && !skip_fixup) {
     // tiles the fused kernel declined (queued in fbq, status TDBG_E_FALLBACK)
     // are redone by the general interpreter, same stream, no host round trip;
@@ -838,12 +857,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     // declined (malformed or unusual ones): a small grid, whose dispatch is
     // most of an empty fixup launch's cost
     const uint32_t fgrid = std::min<uint32_t>(ggrid, streamed ? 32u : (uint32_t)c->cus);
+    if (te) tdbg::ev_arm.stop = te[2];
     e = tdbg_launch_fixup(&g, fgrid, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
     if (streamed) c->sq_clean = true;
   }
   if (te) {
-    HIP_OK(hipEventRecord(te[2], stream));
+    if (!queued || skip_fixup) HIP_OK(hipEventRecord(te[2], stream));
     c->last_te = (int64_t)(te - c->tev.data());
   }
   return TDBG_OK;

@@ -18,6 +18,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_general.h"
 
@@ -92,13 +93,13 @@ unfilter_fixup_kernel(const KParams kp) {
 // ---------------------------------------------------------------------------
 extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid,
                                           hipStream_t stream) {
-  hipLaunchKernelGGL(tdbg::unfilter_general_kernel, dim3(grid), dim3(GEN_NT), 0, stream, *kp);
+  TDBG_LAUNCH(tdbg::unfilter_general_kernel, dim3(grid), dim3(GEN_NT), stream, *kp);
   return hipGetLastError();
 }
 
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream) {
-  hipLaunchKernelGGL(tdbg::unfilter_fixup_kernel, dim3(grid), dim3(GEN_NT), 0, stream, *kp);
+  TDBG_LAUNCH(tdbg::unfilter_fixup_kernel, dim3(grid), dim3(GEN_NT), stream, *kp);
   return hipGetLastError();
 }
 

@@ -51,6 +51,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
 
@@ -815,6 +816,6 @@ extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid,
   auto k = stm == 3 ? unfilter_stream_kernel<true, 3, 4>
            : sgn    ? (pb1 ? unfilter_stream_kernel<true, 1, 1> : unfilter_stream_kernel<true, 1, 4>)
                     : (pb1 ? unfilter_stream_kernel<false, 1, 1> : unfilter_stream_kernel<false, 1, 4>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
+  TDBG_LAUNCH(k, dim3(grid), dim3(NT), s, *kp);
   return hipGetLastError();
 }

@@ -42,6 +42,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
 
@@ -533,6 +534,6 @@ extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t g
                   : abl == 4 ? unfilter_stream_raw_kernel<true, 4>
                              : unfilter_stream_raw_kernel<true, 0>)
                : unfilter_stream_raw_kernel<false, 0>;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), 0, s, *kp);
+  TDBG_LAUNCH(k, dim3(grid), dim3(NT), s, *kp);
   return hipGetLastError();
 }

@@ -22,6 +22,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 
 namespace tdbg {
 namespace shf {
@@ -99,6 +100,6 @@ extern "C" hipError_t tdbg_launch_stream_shuffle4(const tdbg::KParams* kp, hipSt
   using namespace tdbg::shf;
   const uint64_t grid = kp->ntiles * PARTS;
   if (grid == 0 || grid > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(unfilter_shuffle4_kernel, dim3((uint32_t)grid), dim3(NT), 0, s, *kp);
+  TDBG_LAUNCH(unfilter_shuffle4_kernel, dim3((uint32_t)grid), dim3(NT), s, *kp);
   return hipGetLastError();
 }

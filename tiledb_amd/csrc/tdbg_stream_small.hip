@@ -50,6 +50,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
 
@@ -682,13 +683,13 @@ extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t
                                                hipStream_t s) {
   using namespace tdbg::ssm;
   if (mode == M_DD) {
-    hipLaunchKernelGGL((unfilter_stream_small_kernel<M_DD, false>), dim3(grid), dim3(NT), 0, s, *kp);
+    TDBG_LAUNCH((unfilter_stream_small_kernel<M_DD, false>), dim3(grid), dim3(NT), s, *kp);
   } else if (mode == M_RLE) {
-    hipLaunchKernelGGL((unfilter_stream_small_kernel<M_RLE, false>), dim3(grid), dim3(NT), 0, s, *kp);
+    TDBG_LAUNCH((unfilter_stream_small_kernel<M_RLE, false>), dim3(grid), dim3(NT), s, *kp);
   } else if (sgn) {
-    hipLaunchKernelGGL((unfilter_stream_small_kernel<M_PDBWR, true>), dim3(grid), dim3(NT), 0, s, *kp);
+    TDBG_LAUNCH((unfilter_stream_small_kernel<M_PDBWR, true>), dim3(grid), dim3(NT), s, *kp);
   } else {
-    hipLaunchKernelGGL((unfilter_stream_small_kernel<M_PDBWR, false>), dim3(grid), dim3(NT), 0, s, *kp);
+    TDBG_LAUNCH((unfilter_stream_small_kernel<M_PDBWR, false>), dim3(grid), dim3(NT), s, *kp);
   }
   return hipGetLastError();
 }
