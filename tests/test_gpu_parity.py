@@ -606,3 +606,69 @@ def test_chunk_stream_multichunk(eng, ctx, oracle_mod, variant):
     for i in range(n):
         o = int(batch.out_off[i])
         assert np.array_equal(out[o:o + vals[i % 6].nbytes], vals[i % 6].view(np.uint8)), f"tile {i}"
+
+
+def _chunk_headers(t):
+    """(offset, orig, fl, ml) of every chunk header of a filtered tile (tile.cc:280-313)."""
+    n = int(np.frombuffer(t[:8].tobytes(), dtype=np.uint64)[0])
+    o, hs = 8, []
+    for _ in range(n):
+        orig, fl, ml = (int(x) for x in np.frombuffer(t[o:o + 12].tobytes(), dtype=np.uint32))
+        hs.append((o, orig, fl, ml))
+        o += 12 + ml + fl
+    return hs
+
+
+@pytest.mark.parametrize("variant", ["active", "rand"])
+def test_chunk_stream_walk_rejects(eng, ctx, oracle_mod, variant):
+    """Chunk mode: tiles whose chunk walk fails (a chunk's data or metadata
+    size past the tile end, a chunk count one too high or one too low, an
+    unfiltered size that no longer sums to the tile) among good 16-chunk
+    tiles.  The directory counts chunks from the tile header and rejects on
+    its single walk (tdbg_chunkdir.hip): statuses are the oracle's, a
+    rejected tile's output keeps the fill bytes (no kernel takes its
+    records), good tiles are bit-exact and all their full chunks stream."""
+    import workloads as W
+    from tiledb_amd.filter_pipeline import Datatype
+    ser = W.c5_pipeline_bytes()
+    op = oracle_mod.OraclePipeline(ser, 23, int(Datatype.INT32), 4)
+    dp = eng.DevicePipeline(ser, 23, int(Datatype.INT32), 4)
+    rng = np.random.default_rng(33)
+    v = np.concatenate([W.c5_values(variant, c, rng) for c in range(16)])
+    good = np.frombuffer(op.filter_tile(v.view(np.uint8)), dtype=np.uint8)
+    hs = _chunk_headers(good)
+    assert len(hs) == 16
+
+    def put32(t, o, x):
+        t[o:o + 4] = np.frombuffer(np.uint32(x).tobytes(), dtype=np.uint8)
+
+    def mutate(k):
+        t = good.copy()
+        if k == 1:
+            put32(t, hs[5][0] + 4, 0x7fffffff)      # chunk 5's data size past the end
+        elif k == 2:
+            put32(t, hs[9][0] + 8, 0x7fffffff)      # chunk 9's metadata size past the end
+        elif k == 3:
+            t[:8] = np.frombuffer(np.uint64(17).tobytes(), dtype=np.uint8)  # one chunk too many
+        elif k == 4:
+            t[:8] = np.frombuffer(np.uint64(15).tobytes(), dtype=np.uint8)  # one too few
+        elif k == 5:
+            put32(t, hs[7][0], hs[7][1] + 4)         # chunk 7's unfiltered size
+        return t
+
+    tiles = [mutate(k % 6) for k in range(36)]
+    osz = [v.nbytes] * len(tiles)
+    batch = eng.TileBatch.from_host(tiles, osz, fill=0x5A, align=16)
+    c0 = ctx.stream_chunks()
+    st = ctx.unfilter(dp, batch, chunk_parallel=True)
+    out = batch.outputs_host()
+    for i, t in enumerate(tiles):
+        rc, ref = op.unfilter_tile(t, osz[i], fill=0x5A)
+        assert int(st[i]) == rc, f"tile {i} (mutation {i % 6}): gpu {st[i]} oracle {rc}"
+        o = int(batch.out_off[i])
+        if i % 6 == 0:
+            assert rc == 0 and np.array_equal(out[o:o + osz[i]], ref), f"tile {i}"
+        else:
+            assert rc != 0
+            assert (out[o:o + osz[i]] == 0x5A).all(), f"tile {i}: a rejected tile's output was written"
+    assert ctx.stream_chunks() - c0 == 16 * (len(tiles) // 6)

@@ -40,7 +40,7 @@ extern "C" hipError_t tdbg_launch_filter_shuffle4(const tdbg::KParams* kp, uint3
                                                   hipStream_t s);
 extern "C" hipError_t tdbg_launch_chunk_dir(const tdbg::KParams* kp, uint32_t* cnt, uint32_t* base,
                                             tdbg::ChunkRec* recs, uint32_t cap, uint32_t* total,
-                                            uint64_t* need, hipStream_t stream);
+                                            uint64_t* need, uint32_t* cq, hipStream_t stream);
 extern "C" hipError_t tdbg_launch_extra_offset(uint64_t ntiles, uint8_t* const* out, const uint64_t* out_size,
                                                const uint64_t* var_size, const int32_t* status,
                                                hipStream_t stream);
@@ -707,7 +707,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // thread (it runs before the fused kernel that appends).  The streaming
   // kernel's own queue count was reset by the last streamed launch's fixup
   // kernel (or is reset here): two memset launches fewer per C5 launch.
-  if (queued && !streamed) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
+  // (chunked: the directory pass starts the queue counts)
+  if (queued && !streamed && !chunked) HIP_OK(hipMemsetAsync(kp.fbq, 0, sizeof(uint32_t), stream));
   if (streamed && !c->sq_clean) HIP_OK(hipMemsetAsync(c->d_sq, 0, sizeof(uint32_t), stream));
   if (streamed) c->sq_clean = false;  // until this launch's fixup is enqueued
   if (chunked) {
@@ -744,25 +745,24 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       }
     }
     if (!c->dir_total) HIP_OK(hipMalloc(&c->dir_total, 4));
+    const bool cq_used = (c5_stream || small_mode >= 0) && !no_stream && !d_list;
+    if (cq_used && c->cq_cap < c->dir_cap) {
+      // the streaming kernels take the directory's chunk records; their
+      // queue holds chunk indices
+      HIP_OK(hipStreamSynchronize(stream));  // an earlier launch may still read the old queue
+      if (c->d_cq) HIP_OK(hipFree(c->d_cq));
+      c->d_cq = nullptr;
+      c->cq_cap = 0;
+      HIP_OK(hipMalloc(&c->d_cq, (c->dir_cap + 1) * sizeof(uint32_t)));
+      c->cq_cap = c->dir_cap;
+    }
+    // (zeroes the fallback queue's and the chunk queue's counts first)
     hipError_t e = tdbg_launch_chunk_dir(&kp, c->dir_cnt, c->dir_base, c->dir_recs,
                                          (uint32_t)std::min<uint64_t>(c->dir_cap, 0xffffffffull), c->dir_total,
-                                         c->dir_need_dev, stream);
+                                         c->dir_need_dev, cq_used ? c->d_cq : nullptr, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("chunk directory launch: ") + hipGetErrorString(e));
     kp.chunks = c->dir_recs;
     kp.nchunks = c->dir_total;
-    if ((c5_stream || small_mode >= 0) && !no_stream && !d_list) {
-      // the streaming kernels take the directory's chunk records; their
-      // queue holds chunk indices
-      if (c->cq_cap < c->dir_cap) {
-        HIP_OK(hipStreamSynchronize(stream));  // an earlier launch may still read the old queue
-        if (c->d_cq) HIP_OK(hipFree(c->d_cq));
-        c->d_cq = nullptr;
-        c->cq_cap = 0;
-        HIP_OK(hipMalloc(&c->d_cq, (c->dir_cap + 1) * sizeof(uint32_t)));
-        c->cq_cap = c->dir_cap;
-      }
-      HIP_OK(hipMemsetAsync(c->d_cq, 0, sizeof(uint32_t), stream));
-    }
   }
   // the headline pipeline's streaming kernels on chunk records (chunk-parallel
   // launches of multi-chunk tiles, SURVEY 8(a) FilterPipeline::run_reverse's
@@ -853,10 +853,10 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     tdbg::KParams g = kp;
     g.fixup = 1;
     g.sq = streamed ? c->d_sq : nullptr;  // the fixup resets the streaming queue's count
-    // After a streamed launch the queue holds only tiles both fast kernels
-    // declined (malformed or unusual ones): a small grid, whose dispatch is
-    // most of an empty fixup launch's cost
-    const uint32_t fgrid = std::min<uint32_t>(ggrid, streamed ? 32u : (uint32_t)c->cus);
+    // After a streamed launch (tiles or chunk records) the queue holds only
+    // tiles both fast kernels declined (malformed or unusual ones): a small
+    // grid, whose dispatch is most of an empty fixup launch's cost
+    const uint32_t fgrid = std::min<uint32_t>(ggrid, (streamed || chunk_stream) ? 32u : (uint32_t)c->cus);
     if (te) tdbg::ev_arm.stop = te[2];
     e = tdbg_launch_fixup(&g, fgrid, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
