@@ -62,7 +62,11 @@ constexpr uint32_t JU = 128;         // output units per job
 constexpr uint32_t NJOB = 1024 / JU; // jobs per wave and tile
 constexpr uint32_t RU = 33;          // 16-B DMA units per job plane (512 B at any alignment)
 constexpr uint32_t RW = (RU + 1) * 4;  // dwords per job plane region (+1 unit: reads past the range)
-constexpr int NB = 2;                // job buffers per wave
+#ifndef TDBG_RAW_NB
+#define TDBG_RAW_NB 2
+#endif
+constexpr int NB = TDBG_RAW_NB;      // job buffers per wave (2 or 3)
+static_assert(NB == 2 || NB == 3, "job buffers");
 
 struct Lds {
   uint32_t PF[PFU * 4];
@@ -382,14 +386,31 @@ __device__ __forceinline__ void job_fast(const Lds& L, const Job& jb, const uint
     }
 }
 
-// The wave's 1,024 output units of one tile, in NJOB jobs of JU units, job
-// buffers double-buffered.  VMEM issue order per wave (D = one job's 4 DMA
-// instructions, S = its 2 stores):
-//   D0 D1 | j0 D2 S0 | j1 D3 S1 | j2 D4 S2 | ... | j5 D7 S5 | j6 S6 | j7 S7
-// so job i waits until only the operations issued after D_i are left:
-// i = 0: D1 (4); i = 1: D2 S0 (6); 2 <= i <= 6: S(i-2) D(i+1) S(i-1) (8, i = 6:
-// S4 D7 S5); i = 7: S5 S6 (4).  No other VMEM instruction is issued meanwhile
-// (no scratch: the build's resource check keeps ScratchSize at 0).
+// VMEM operations a wave has issued after job i's DMA when job i waits
+// (issue order: D_0 .. D_{NB-1}, then per job i: its compute, D_{i+NB},
+// its stores S_i; D = 4 DMA instructions, S = 2 stores): the D_k with
+// i < k <= min(i + NB - 1, NJOB - 1), and the S_j with i - NB <= j < i.
+constexpr uint32_t vm_after(uint32_t i) {
+  return 4 * ((i + NB - 1 < NJOB - 1 ? i + NB - 1 : NJOB - 1) - i) + 2 * (i < (uint32_t)NB ? i : (uint32_t)NB);
+}
+
+// s_waitcnt vmcnt(n) for the counts vm_after takes (n uniform)
+__device__ __forceinline__ void vm_wait(uint32_t n) {
+  switch (n) {
+#define TDBG_VMW(c) \
+  case c: asm volatile("s_waitcnt vmcnt(" #c ")" ::: "memory"); break;
+    TDBG_VMW(4) TDBG_VMW(6) TDBG_VMW(8) TDBG_VMW(10) TDBG_VMW(12) TDBG_VMW(14)
+#undef TDBG_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+static_assert(vm_after(0) >= 4 && vm_after(NJOB - 1) >= 4 && vm_after(3) <= 14, "vm_wait cases");
+
+// The wave's 1,024 output units of one tile, in NJOB jobs of JU units, NB
+// job buffers in a ring: job i waits until only the operations issued after
+// its DMA are left (vm_after; NB = 2: 4, 6, 8 x 5, 4).  No other VMEM
+// instruction is issued meanwhile (no scratch: the build's resource check
+// keeps ScratchSize at 0).
 template <bool SGN, int ABL>
 __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uint32_t l, uint32_t wsh) {
   const uint32_t esh = wsh - 2;
@@ -398,12 +419,12 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
   const Setup st = wave_setup<ABL>(L, d, w, wsh, l);
   Job jc = job_dma(st, 0, rbase, l);
   Job jn = job_dma(st, 1, rbase + RB, l);
+  Job jn2 = jn;
+  if constexpr (NB == 3) jn2 = job_dma(st, 2, rbase + 2 * RB, l);
   for (uint32_t i = 0; i < NJOB; i++) {
-    const uint32_t buf = i & 1;
+    const uint32_t buf = i % NB;
     const uint32_t J = 1024 * w + JU * i;
-    if (i == 0 || i == NJOB - 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (i == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    vm_wait(vm_after(i));
     const uint32_t* R0 = &L.J[w][buf][0][0];
     uint32_t x[2][4];
     if (jc.gen == 0) {
@@ -425,9 +446,9 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
     v4u y[2];
 #pragma unroll
     for (int u = 0; u < 2; u++) y[u] = unshuffle4(x[u]);
-    // the buffer's reads are consumed: job i + 2's DMA may overwrite it
+    // the buffer's reads are consumed: job i + NB's DMA may overwrite it
     Job jw = jc;
-    if (i + 2 < NJOB) jw = job_dma(st, i + 2, rbase + buf * RB, l);
+    if (i + NB < NJOB) jw = job_dma(st, i + NB, rbase + buf * RB, l);
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       g_u4* dst = (g_u4*)(d.out + 16u * (J + 64 * u + l));
@@ -438,7 +459,12 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
       }
     }
     jc = jn;
-    jn = jw;
+    if constexpr (NB == 3) {
+      jn = jn2;
+      jn2 = jw;
+    } else {
+      jn = jw;
+    }
   }
 }
 
