@@ -711,8 +711,9 @@ def main():
                 "tiles": args.shard_tiles, "steps": args.steps, "variants": sh,
                 "min_over_variants_GiBps": round(min(x["GiBps"] for x in sh.values()), 2),
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sh.values()), 4)}
-    if rank == 0 and not args.no_cpu_baseline:
-        # after every timed region, at any N (rank 0 only)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # after every timed region, at N = 1 only (the N > 1 lines divide the
+        # same job over more GPUs; the CPU figure does not change with N)
         line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds, scaling=True)
     if rank == 0:
         print(json.dumps(line))
