@@ -107,7 +107,7 @@ def test_fused_spec_no_fallback(eng, ctx, oracle_mod, case, align):
     del dp
 
 
-def check_parity_replicated(eng, ctx, O, case, enc, n, align=1):
+def check_parity_replicated(eng, ctx, O, case, enc, n, align=1, chunk_parallel=False):
     """n tiles cycling over the unique encoded tiles `enc` (the oracle runs
     once per unique tile): a launch of more tiles than the GPU has CUs, so it
     takes the tile-serial path (fused kernel: cross-tile prefetch and the
@@ -117,7 +117,7 @@ def check_parity_replicated(eng, ctx, O, case, enc, n, align=1):
     refs = [op.unfilter_tile(e[0], e[2], case.offsets_tile) for e in enc]
     idx = np.arange(n) % len(enc)
     batch = eng.TileBatch.from_host([enc[i][0] for i in idx], [enc[i][2] for i in idx], align=align)
-    st = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile)
+    st = ctx.unfilter(dp, batch, offsets_tiles=case.offsets_tile, chunk_parallel=chunk_parallel)
     out = batch.outputs_host()
     for k, i in enumerate(idx):
         rc, ref = refs[i]
@@ -672,3 +672,21 @@ def test_chunk_stream_walk_rejects(eng, ctx, oracle_mod, variant):
             assert rc != 0
             assert (out[o:o + osz[i]] == 0x5A).all(), f"tile {i}: a rejected tile's output was written"
     assert ctx.stream_chunks() - c0 == 16 * (len(tiles) // 6)
+
+
+@pytest.mark.parametrize("case", _CONFIG, ids=[c.name for c in _CONFIG])
+def test_chunk_parallel_many_tiles(eng, ctx, oracle_mod, case):
+    """A chunk-parallel launch of more than 4,096 tiles (the directory's
+    parallel header-count launch, tdbg_chunkdir.hip) with corrupted tiles
+    among them (a chunk count past the tile, a chunk data size past the
+    end): statuses and bytes as the oracle's."""
+    _, enc = encode(oracle_mod, case)
+    assert enc
+    f = np.frombuffer(bytes(enc[0][0]), dtype=np.uint8).copy()
+    bad_count = f.copy()
+    bad_count[:8] = 0x7f
+    bad_fl = f.copy()
+    bad_fl[12:16] = 0xff  # chunk 0's filtered size
+    enc = list(enc) + [(bad_count, None, enc[0][2]), (bad_fl, None, enc[0][2])]
+    st = check_parity_replicated(eng, ctx, oracle_mod, case, enc, 4500, chunk_parallel=True)
+    assert (st != 0).sum() >= 2 * (4500 // len(enc))
