@@ -506,7 +506,8 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
   }
   // the fused kernel's fallback queue starts empty for this launch (it runs
   // next on the same stream and is the only one to append; chunk mode: the
-  // host cleared it before the directory pass, which may append)
+  // directory's scan kernel cleared it, and may have appended, so fbq is
+  // not passed here)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const bool chunked = kp.chunks != nullptr;
   const uint32_t w = wave_();

@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
   const bool chunked = kp.chunks != nullptr;
   // the fused kernel's fallback queue starts empty for this launch (it runs
   // next on the same stream and is the only one to append; chunk mode: the
-  // host cleared it before the directory pass)
+  // directory's scan kernel cleared it, and fbq is not passed here)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const uint32_t w = wave_();
   uint64_t ok_tiles = 0;
