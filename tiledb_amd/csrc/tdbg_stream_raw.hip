@@ -51,8 +51,17 @@ namespace sraw {
 
 using namespace sc;
 
-constexpr int NT = 256;  // 4 wave64 per workgroup
-constexpr int NWV = NT / 64;
+#ifndef TDBG_RAW_PW
+#define TDBG_RAW_PW 0
+#endif
+// PW: a fifth wave per workgroup (the parser) DMAs and parses tile n + 1's
+// prefix while the four job waves decode tile n: one barrier per tile, and the
+// parse is off the job waves' path.  Otherwise wave 0 parses between two
+// barriers while the other waves wait.
+constexpr bool PW = TDBG_RAW_PW != 0;
+constexpr int NWV = 4;                    // job waves (wave64)
+constexpr int NT = 64 * (NWV + (PW ? 1 : 0));
+constexpr int NS = PW ? 2 : 1;            // window-table slots
 constexpr uint32_t OUTB = 65536;     // output bytes per tile (one 64 KiB chunk of int32)
 constexpr uint32_t SMALL = CODED_CAP;  // tiles this big or smaller belong to tdbg_stream.hip
 constexpr uint32_t PFU = 256;        // prefix: 256 16-B units
@@ -70,9 +79,9 @@ static_assert(NB == 2 || NB == 3, "job buffers");
 
 struct Lds {
   uint32_t PF[PFU * 4];
-  uint2 TAB[TABN];             // {image offset of the window's data | kind << 20, window minimum}
+  uint2 TAB[NS][TABN];         // {image offset of the window's data | kind << 20, window minimum}
   uint32_t J[NWV][NB][4][RW];  // per wave, buffer and plane: the job's compressed plane bytes
-  uint32_t hd[4];              // published by wave 0: verdict, log2(window bytes), nwin - 1
+  uint32_t hd[NS][4];          // published by the parse: verdict, log2(window bytes), nwin - 1
 };
 
 // bytes [o, o + 4) of a dword array (any alignment)
@@ -144,16 +153,22 @@ __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
 // m + ml + 28 <= 35 + 8 + 9 * 320 + 24 + 28 < 3 KiB - 16 (nwin <= TABN), so
 // the rest of PF may hold the last tile's bytes; staging only what the parse
 // reads keeps the re-read of window 0's data (the jobs DMA it again) small.
+// (PW: the parser wave issues all three, so its own vmcnt covers the prefix)
 __device__ __forceinline__ void prefix_dma(Lds& L, const Desc& d, uint32_t w, uint32_t l) {
   const uint64_t a0 = (uint64_t)d.in & ~15ull;
-  if (w < 3) dma16(a0 + 16ull * (64 * w + l), lds_addr(L.PF) + 1024 * w);
+  if constexpr (PW) {
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) dma16(a0 + 16ull * (64 * k + l), lds_addr(L.PF) + 1024 * k);
+  } else {
+    if (w < 3) dma16(a0 + 16ull * (64 * w + l), lds_addr(L.PF) + 1024 * w);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // header parse (wave 0): tile/chunk header, window table, frame, DD headers
 // ---------------------------------------------------------------------------
 template <bool SGN>
-__device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool chunked) {
+__device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool chunked, uint32_t slot) {
   const uint32_t* P = L.PF;
   // the chunk header follows the tile's u64 chunk count, or (chunk mode:
   // a chunk of a multi-chunk tile) starts the image
@@ -202,7 +217,7 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
 #pragma unroll
     for (int q = 0; q < 5; q++) {
       const uint32_t wi = 5 * l + q;
-      if (wi < nwin) L.TAB[wi] = make_uint2(off | (kind[q] << 20), mn[q]);
+      if (wi < nwin) L.TAB[slot][wi] = make_uint2(off | (kind[q] << 20), mn[q]);
       off += cs[q];
     }
   }
@@ -227,9 +242,9 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   ok = ok && at(1) == 2 && at(5) == 0 && at(9) == 1 && at(13) == OUTB && (at(17) & 0xffu) >= 31 &&
        at(18) == OUTB / 4 && at(22) == 0;
   if (l == 0) {
-    L.hd[0] = ok ? 1u : 0u;
-    L.hd[1] = 31 - __builtin_clz(ws);
-    L.hd[2] = nwin - 1;
+    L.hd[slot][0] = ok ? 1u : 0u;
+    L.hd[slot][1] = 31 - __builtin_clz(ws);
+    L.hd[slot][2] = nwin - 1;
   }
 }
 
@@ -263,11 +278,11 @@ struct Setup {
 };
 
 template <int ABL>
-__device__ __forceinline__ Setup wave_setup(const Lds& L, const Desc& d, uint32_t w, uint32_t wsh, uint32_t l) {
+__device__ __forceinline__ Setup wave_setup(const uint2* TAB, const Desc& d, uint32_t w, uint32_t wsh, uint32_t l) {
   const uint32_t i = (l >> 2) & 7, k = l & 3;
   const uint32_t Q0 = 26 + 16384 * k + 4 * (1024 * w + JU * i);
   const uint32_t W0 = Q0 >> wsh, W1 = (Q0 + 511) >> wsh;  // W1 - W0 <= 2 (windows >= 256 B)
-  const uint32_t xA = L.TAB[W0].x, xB = L.TAB[W0 + 1 < W1 ? W0 + 1 : W1].x, xL = L.TAB[W1].x;
+  const uint32_t xA = TAB[W0].x, xB = TAB[W0 + 1 < W1 ? W0 + 1 : W1].x, xL = TAB[W1].x;
   const uint32_t kA = xA >> 20, kB = xB >> 20, kL = xL >> 20;
   const bool all8 = kA == 0 && kB == 0 && kL == 0, allraw = kA == 2 && kB == 2 && kL == 2;
   Setup st;
@@ -314,14 +329,14 @@ __device__ __forceinline__ Job job_dma(const Setup& st, uint32_t i, uint32_t R0,
 // [Q0 + 4 v, +4) = the upper half of element e = (Q0 + 4 v) / 4 and the
 // lower half of e + 1 (Q0 = 2 mod 4), each looked up in the window table.
 template <bool SGN>
-__device__ __forceinline__ uint32_t dword_general(const Lds& L, const uint32_t* R, uint32_t rb, uint32_t Q0,
+__device__ __forceinline__ uint32_t dword_general(const uint2* TAB, const uint32_t* R, uint32_t rb, uint32_t Q0,
                                                   uint32_t v, uint32_t esh) {
   const uint32_t e = (Q0 >> 2) + v;
   uint32_t val[2];
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     const uint32_t ei = e + i, wi = ei >> esh;
-    const uint2 te = L.TAB[wi];
+    const uint2 te = TAB[wi];
     const uint32_t kind = te.x >> 20;
     const uint32_t o = (te.x & OFFM) + ((ei - (wi << esh)) << kind) - rb;
     const uint32_t x = rd32(R, o);
@@ -349,7 +364,7 @@ __device__ __forceinline__ v4u unshuffle4(const uint32_t (&x)[4]) {
 // windows, so one compressed byte per element in order): elements e and
 // e + 1 are the bytes at rel + v and rel + v + 1.
 template <bool SGN, int K8>
-__device__ __forceinline__ void job_fast(const Lds& L, const Job& jb, const uint32_t* R0, uint32_t J, uint32_t esh,
+__device__ __forceinline__ void job_fast(const uint2* TAB, const Job& jb, const uint32_t* R0, uint32_t J, uint32_t esh,
                                          uint32_t l, uint32_t (&x)[2][4]) {
   uint32_t lo[2][4], hi[2][4], ma[2][4], mb[2][4];
 #pragma unroll
@@ -366,8 +381,8 @@ __device__ __forceinline__ void job_fast(const Lds& L, const Job& jb, const uint
       hi[u][k] = R[(o >> 2) + 1];
       if (b8) {
         const uint32_t e = ((26 + 16384 * k + 4 * J) >> 2) + v;
-        ma[u][k] = L.TAB[e >> esh].y;
-        mb[u][k] = L.TAB[(e + 1) >> esh].y;
+        ma[u][k] = TAB[e >> esh].y;
+        mb[u][k] = TAB[(e + 1) >> esh].y;
       }
     }
 #pragma unroll
@@ -412,11 +427,12 @@ static_assert(vm_after(0) >= 4 && vm_after(NJOB - 1) >= 4 && vm_after(3) <= 14, 
 // instruction is issued meanwhile (no scratch: the build's resource check
 // keeps ScratchSize at 0).
 template <bool SGN, int ABL>
-__device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uint32_t l, uint32_t wsh) {
+__device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uint32_t l, uint32_t wsh, uint32_t slot) {
+  const uint2* TAB = L.TAB[slot];
   const uint32_t esh = wsh - 2;
   const uint32_t rbase = lds_addr(&L.J[w][0][0][0]);
   constexpr uint32_t RB = 4 * RW * 4;  // bytes per job buffer
-  const Setup st = wave_setup<ABL>(L, d, w, wsh, l);
+  const Setup st = wave_setup<ABL>(TAB, d, w, wsh, l);
   Job jc = job_dma(st, 0, rbase, l);
   Job jn = job_dma(st, 1, rbase + RB, l);
   Job jn2 = jn;
@@ -430,7 +446,7 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
     if (jc.gen == 0) {
       switch (jc.k8) {
 #define TDBG_K8(m) \
-  case m: job_fast<SGN, m>(L, jc, R0, J, esh, l, x); break;
+  case m: job_fast<SGN, m>(TAB, jc, R0, J, esh, l, x); break;
         TDBG_K8(0) TDBG_K8(1) TDBG_K8(2) TDBG_K8(3) TDBG_K8(4) TDBG_K8(5) TDBG_K8(6) TDBG_K8(7)
         TDBG_K8(8) TDBG_K8(9) TDBG_K8(10) TDBG_K8(11) TDBG_K8(12) TDBG_K8(13) TDBG_K8(14) TDBG_K8(15)
 #undef TDBG_K8
@@ -441,7 +457,7 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
       for (int u = 0; u < 2; u++)
 #pragma unroll
         for (int k = 0; k < 4; k++)
-          x[u][k] = dword_general<SGN>(L, R0 + k * RW, jc.rb[k], 26 + 16384 * k + 4 * J, 64 * u + l, esh);
+          x[u][k] = dword_general<SGN>(TAB, R0 + k * RW, jc.rb[k], 26 + 16384 * k + 4 * J, 64 * u + l, esh);
     }
     v4u y[2];
 #pragma unroll
@@ -469,7 +485,11 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
 }
 
 #ifndef TDBG_RAW_OCC
+#if TDBG_RAW_PW
+#define TDBG_RAW_OCC 4  // workgroups per CU (5 waves each at <= 96 VGPRs)
+#else
 #define TDBG_RAW_OCC 5  // workgroups per CU (<= 96 VGPRs, 24 KB LDS each)
+#endif
 #endif
 
 // ABL: timing ablations (outputs not meaningful): 1 parse only a workgroup's
@@ -497,6 +517,54 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
     }
     decline(kp, cur.t);
   }
+  if constexpr (PW) {
+    // the parser wave (w == NWV) is one tile ahead: tile n + 1's prefix DMA
+    // and parse (into the other window-table slot) run while the job waves
+    // decode tile n; one barrier per tile publishes the slot and frees the
+    // one just used
+    const bool parser = w == NWV;
+    uint32_t slot = 0;
+    if (have && parser) {
+      prefix_dma(L, cur, w, l);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      parse<SGN>(L, cur, l, chunked, 0);
+    }
+    lds_barrier();
+    while (have) {
+      Desc nxt{};
+      bool hn = false;
+      while (walk_next(kp, wk, it, nxt)) {
+        it++;
+        if (takes(kp, nxt)) {
+          hn = true;
+          break;
+        }
+        decline(kp, nxt.t);
+      }
+      if (parser) {
+        if (hn) {
+          prefix_dma(L, nxt, w, l);  // PF: only this wave reads it, and its last parse is done
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          parse<SGN>(L, nxt, l, chunked, slot ^ 1);
+        }
+      } else {
+        const bool ok = __builtin_amdgcn_readfirstlane(L.hd[slot][0]) != 0;
+        const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[slot][1]);
+        if (ok) {
+          if (ABL != 4) tile_jobs<SGN, ABL>(L, cur, w, l, wsh, slot);
+          ok_tiles++;
+          if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
+        } else {
+          decline(kp, cur.t);
+        }
+      }
+      lds_barrier();
+      slot ^= 1;
+      cur = nxt;
+      have = hn;
+    }
+    have = false;  // (the two-barrier loop below is not taken)
+  }
   if (have) prefix_dma(L, cur, w, l);
   bool pf_waited = false;
   while (have) {
@@ -514,16 +582,16 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
     if (ABL != 1 || ok_tiles == 0) {
       if (!pf_waited) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();  // B1: the prefix has landed; the last tile's jobs are done with TAB
-      if (w == 0) parse<SGN>(L, cur, l, chunked);
+      if (w == 0) parse<SGN>(L, cur, l, chunked, 0);
       lds_barrier();  // B2: window table and verdict
     }
-    const bool ok = __builtin_amdgcn_readfirstlane(L.hd[0]) != 0;
-    const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
+    const bool ok = __builtin_amdgcn_readfirstlane(L.hd[0][0]) != 0;
+    const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[0][1]);
     // PF is free (only wave 0 read it, before B2): the next tile's prefix
     if (hn && ABL != 1) prefix_dma(L, nxt, w, l);
     pf_waited = false;
     if (ok) {
-      if (ABL != 4) tile_jobs<SGN, ABL>(L, cur, w, l, wsh);
+      if (ABL != 4) tile_jobs<SGN, ABL>(L, cur, w, l, wsh, 0);
       pf_waited = true;  // the first job's wait covered the prefix (older)
       ok_tiles++;
       if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
