@@ -67,9 +67,15 @@ constexpr uint32_t SMALL = CODED_CAP;  // tiles this big or smaller belong to td
 constexpr uint32_t PFU = 256;        // prefix: 256 16-B units
 constexpr uint32_t TABN = 320;       // BWR windows per chunk
 constexpr uint32_t LBWR = 65562;     // BWR output bytes of a raw-DD C5 chunk: 17 + 9 + 65536
-constexpr uint32_t JU = 128;         // output units per job
+#ifndef TDBG_RAW_JU
+#define TDBG_RAW_JU 128
+#endif
+constexpr uint32_t JU = TDBG_RAW_JU; // output units per job (128, or 256: 1 KiB plane ranges)
+static_assert(JU == 128 || JU == 256, "job size");
 constexpr uint32_t NJOB = 1024 / JU; // jobs per wave and tile
-constexpr uint32_t RU = 33;          // 16-B DMA units per job plane (512 B at any alignment)
+constexpr uint32_t NU = JU / 64;     // output units per lane and job
+constexpr uint32_t RU = JU / 4 + 1;  // 16-B DMA units per job plane (4 JU bytes at any alignment)
+constexpr uint32_t ND = (RU + 63) / 64;  // DMA instructions per job plane
 constexpr uint32_t RW = (RU + 1) * 4;  // dwords per job plane region (+1 unit: reads past the range)
 #ifndef TDBG_RAW_NB
 #define TDBG_RAW_NB 2
@@ -279,18 +285,23 @@ struct Setup {
 
 template <int ABL>
 __device__ __forceinline__ Setup wave_setup(const uint2* TAB, const Desc& d, uint32_t w, uint32_t wsh, uint32_t l) {
-  const uint32_t i = (l >> 2) & 7, k = l & 3;
+  const uint32_t i = (l >> 2) % NJOB, k = l & 3;
   const uint32_t Q0 = 26 + 16384 * k + 4 * (1024 * w + JU * i);
-  const uint32_t W0 = Q0 >> wsh, W1 = (Q0 + 511) >> wsh;  // W1 - W0 <= 2 (windows >= 256 B)
-  const uint32_t xA = TAB[W0].x, xB = TAB[W0 + 1 < W1 ? W0 + 1 : W1].x, xL = TAB[W1].x;
-  const uint32_t kA = xA >> 20, kB = xB >> 20, kL = xL >> 20;
-  const bool all8 = kA == 0 && kB == 0 && kL == 0, allraw = kA == 2 && kB == 2 && kL == 2;
+  const uint32_t W0 = Q0 >> wsh, W1 = (Q0 + 4 * JU - 1) >> wsh;  // W1 - W0 <= 4 JU / 256 (windows >= 256 B)
+  const uint32_t xA = TAB[W0].x, xL = TAB[W1].x;
+  bool all8 = (xA >> 20) == 0 && (xL >> 20) == 0, allraw = (xA >> 20) == 2 && (xL >> 20) == 2;
+#pragma unroll
+  for (uint32_t q = 1; q < 4 * JU / 256; q++) {
+    const uint32_t kq = TAB[W0 + q < W1 ? W0 + q : W1].x >> 20;
+    all8 = all8 && kq == 0;
+    allraw = allraw && kq == 2;
+  }
   Setup st;
-  const bool mine = l < 32;
+  const bool mine = l < 4 * NJOB;
   st.k8 = __builtin_amdgcn_ballot_w64(mine && all8);
   st.gen = __builtin_amdgcn_ballot_w64(mine && !all8 && !allraw);
   const uint32_t c0 = cpos(xA, W0 << wsh, Q0, false);
-  const uint32_t c1 = cpos(xL, W1 << wsh, Q0 + 511, true);
+  const uint32_t c1 = cpos(xL, W1 << wsh, Q0 + 4 * JU - 1, true);
   const uint64_t g0 = ((uint64_t)d.in + c0) & ~15ull;
   st.nu = ABL == 2 ? 1u : (uint32_t)(((((uint64_t)d.in + c1 + 15) & ~15ull) - g0) >> 4);
   st.g0lo = (uint32_t)g0;
@@ -321,6 +332,11 @@ __device__ __forceinline__ Job job_dma(const Setup& st, uint32_t i, uint32_t R0,
     jb.rel[k] = __builtin_amdgcn_readlane(st.rel, s);
     jb.rb[k] = __builtin_amdgcn_readlane(st.rb, s);
     if (l < nu) dma16(g0 + 16ull * l, R0 + k * (RW * 4));
+    // (JU 256: units 64.. by a second instruction, always issued -- the
+    // counted waits assume ND per plane; with nu <= 64 lane 0 moves unit 0
+    // again into slot 64, which nothing reads)
+    if constexpr (ND > 1)
+      if (l < (nu > 64 ? nu - 64 : 1u)) dma16(nu > 64 ? g0 + 16ull * (64 + l) : g0, R0 + k * (RW * 4) + 1024);
   }
   return jb;
 }
@@ -365,10 +381,10 @@ __device__ __forceinline__ v4u unshuffle4(const uint32_t (&x)[4]) {
 // e + 1 are the bytes at rel + v and rel + v + 1.
 template <bool SGN, int K8>
 __device__ __forceinline__ void job_fast(const uint2* TAB, const Job& jb, const uint32_t* R0, uint32_t J, uint32_t esh,
-                                         uint32_t l, uint32_t (&x)[2][4]) {
-  uint32_t lo[2][4], hi[2][4], ma[2][4], mb[2][4];
+                                         uint32_t l, uint32_t (&x)[NU][4]) {
+  uint32_t lo[NU][4], hi[NU][4], ma[NU][4], mb[NU][4];
 #pragma unroll
-  for (int u = 0; u < 2; u++)
+  for (int u = 0; u < (int)NU; u++)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       constexpr int dummy = 0;
@@ -386,7 +402,7 @@ __device__ __forceinline__ void job_fast(const uint2* TAB, const Job& jb, const 
       }
     }
 #pragma unroll
-  for (int u = 0; u < 2; u++)
+  for (int u = 0; u < (int)NU; u++)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const bool b8 = (K8 >> k) & 1;
@@ -403,10 +419,10 @@ __device__ __forceinline__ void job_fast(const uint2* TAB, const Job& jb, const 
 
 // VMEM operations a wave has issued after job i's DMA when job i waits
 // (issue order: D_0 .. D_{NB-1}, then per job i: its compute, D_{i+NB},
-// its stores S_i; D = 4 DMA instructions, S = 2 stores): the D_k with
+// its stores S_i; D = 4 ND DMA instructions, S = NU stores): the D_k with
 // i < k <= min(i + NB - 1, NJOB - 1), and the S_j with i - NB <= j < i.
 constexpr uint32_t vm_after(uint32_t i) {
-  return 4 * ((i + NB - 1 < NJOB - 1 ? i + NB - 1 : NJOB - 1) - i) + 2 * (i < (uint32_t)NB ? i : (uint32_t)NB);
+  return 4 * ND * ((i + NB - 1 < NJOB - 1 ? i + NB - 1 : NJOB - 1) - i) + NU * (i < (uint32_t)NB ? i : (uint32_t)NB);
 }
 
 // s_waitcnt vmcnt(n) for the counts vm_after takes (n uniform)
@@ -414,12 +430,19 @@ __device__ __forceinline__ void vm_wait(uint32_t n) {
   switch (n) {
 #define TDBG_VMW(c) \
   case c: asm volatile("s_waitcnt vmcnt(" #c ")" ::: "memory"); break;
-    TDBG_VMW(4) TDBG_VMW(6) TDBG_VMW(8) TDBG_VMW(10) TDBG_VMW(12) TDBG_VMW(14)
+    TDBG_VMW(4) TDBG_VMW(6) TDBG_VMW(8) TDBG_VMW(10) TDBG_VMW(12) TDBG_VMW(14) TDBG_VMW(16) TDBG_VMW(20)
+    TDBG_VMW(24)
 #undef TDBG_VMW
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
-static_assert(vm_after(0) >= 4 && vm_after(NJOB - 1) >= 4 && vm_after(3) <= 14, "vm_wait cases");
+constexpr bool vm_case(uint32_t n) { return n == 4 || n == 6 || (n >= 8 && n <= 16 && n % 2 == 0) || n == 20 || n == 24; }
+constexpr bool vm_cases_ok() {
+  for (uint32_t i = 0; i < NJOB; i++)
+    if (!vm_case(vm_after(i))) return false;
+  return true;
+}
+static_assert(vm_cases_ok(), "vm_wait cases");
 
 // The wave's 1,024 output units of one tile, in NJOB jobs of JU units, NB
 // job buffers in a ring: job i waits until only the operations issued after
@@ -442,7 +465,7 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
     const uint32_t J = 1024 * w + JU * i;
     vm_wait(vm_after(i));
     const uint32_t* R0 = &L.J[w][buf][0][0];
-    uint32_t x[2][4];
+    uint32_t x[NU][4];
     if (jc.gen == 0) {
       switch (jc.k8) {
 #define TDBG_K8(m) \
@@ -454,19 +477,19 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < 2; u++)
+      for (int u = 0; u < (int)NU; u++)
 #pragma unroll
         for (int k = 0; k < 4; k++)
           x[u][k] = dword_general<SGN>(TAB, R0 + k * RW, jc.rb[k], 26 + 16384 * k + 4 * J, 64 * u + l, esh);
     }
-    v4u y[2];
+    v4u y[NU];
 #pragma unroll
-    for (int u = 0; u < 2; u++) y[u] = unshuffle4(x[u]);
+    for (int u = 0; u < (int)NU; u++) y[u] = unshuffle4(x[u]);
     // the buffer's reads are consumed: job i + NB's DMA may overwrite it
     Job jw = jc;
     if (i + NB < NJOB) jw = job_dma(st, i + NB, rbase + buf * RB, l);
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < (int)NU; u++) {
       g_u4* dst = (g_u4*)(d.out + 16u * (J + 64 * u + l));
       if (ABL == 3) {  // timing ablation: stores issued only under a branch never taken (vmcnt counts off: ABL only)
         if (y[u].x == 0x9e3779b9u && y[u].y == 0x7f4a7c15u) __builtin_nontemporal_store(y[u], dst);
@@ -485,8 +508,8 @@ __device__ __forceinline__ void tile_jobs(Lds& L, const Desc& d, uint32_t w, uin
 }
 
 #ifndef TDBG_RAW_OCC
-#if TDBG_RAW_PW
-#define TDBG_RAW_OCC 4  // workgroups per CU (5 waves each at <= 96 VGPRs)
+#if TDBG_RAW_PW || TDBG_RAW_JU > 128
+#define TDBG_RAW_OCC 4  // workgroups per CU (PW: 5 waves each at <= 96 VGPRs; JU 256: 40 KB LDS)
 #else
 #define TDBG_RAW_OCC 5  // workgroups per CU (<= 96 VGPRs, 24 KB LDS each)
 #endif
