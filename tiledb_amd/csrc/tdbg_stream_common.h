@@ -108,13 +108,22 @@ __device__ __forceinline__ uint32_t lds_addr(T* p) {
 // of any address; the kernels wait for it explicitly with counted vmcnt.
 // The instruction is issued iff at least one lane is active: callers count
 // only instructions they know have an active lane.
+// TDBG_DMA_NT: the loads carry the nontemporal hint (experiment builds).
+#ifndef TDBG_DMA_NT
+#define TDBG_DMA_NT 0
+#endif
+#if TDBG_DMA_NT
+#define TDBG_DMA_POLICY " nt"
+#else
+#define TDBG_DMA_POLICY ""
+#endif
 __device__ __forceinline__ void dma16(uint64_t src, uint32_t dst_wave) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off" TDBG_DMA_POLICY "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst_wave))
