@@ -1,0 +1,25 @@
+"""Build provenance of the engine library (tiledb_amd/build.py): the library
+that loads is the one built from this tree's sources."""
+import os
+
+import pytest
+
+from tiledb_amd import build as B
+
+
+def test_source_digest_is_stable_and_covers_every_unit():
+    d1, d2 = B.source_digest(), B.source_digest()
+    assert d1 == d2 and len(d1) == 64
+    srcs = {s for s, _, _ in B.UNITS}
+    assert {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_host.cpp"} <= srcs
+    for s in srcs:
+        assert os.path.exists(os.path.join(B.CSRC, s))
+
+
+@pytest.mark.gpu
+def test_loaded_library_was_built_from_this_tree():
+    # (on the GPU box: the library that travelled with the snapshot matches
+    # the sources next to it, so every GPU result is a result of these sources)
+    pv = B.provenance()
+    assert pv["sources_match"], "libtiledb_amd.so was built from other sources: rebuild (build())"
+    assert pv["library_match"], "libtiledb_amd.so differs from the one its manifest records"

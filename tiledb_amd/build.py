@@ -5,6 +5,8 @@ include/tiledb_amd.h and travels with the repo snapshot to the GPU box.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -13,6 +15,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libtiledb_amd.so")
+# Build provenance: the digest of every source, header and flag the library
+# was built from, written next to it (travels with it to the GPU box, stays
+# out of git like the library).  build() rebuilds whenever the tree's digest
+# differs from the recorded one, not only on a newer mtime.
+MANIFEST = os.path.join(HERE, "libtiledb_amd.build.json")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 
@@ -51,8 +58,32 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_digest() -> str:
+    """sha256 over the library's sources, headers, the C-ABI header and the
+    build flags (arch, fused-spec split, per-unit extra flags)."""
+    h = hashlib.sha256()
+    files = sorted({d for src, _, _ in UNITS for d in _deps(src)})
+    for f in files:
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(json.dumps([ARCH, NPART, [(s, n, e) for s, n, e in UNITS]]).encode())
+    return h.hexdigest()
+
+
+def manifest() -> dict:
+    """The recorded provenance of the built library ({} if none)."""
+    try:
+        with open(MANIFEST) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
 def _stale() -> bool:
-    return _newer(LIB, [d for src, _, _ in UNITS for d in _deps(src)])
+    if _newer(LIB, [d for src, _, _ in UNITS for d in _deps(src)]):
+        return True
+    return manifest().get("sources_sha256") != source_digest()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -104,7 +135,32 @@ def build(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
+    hipcc = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+    with open(MANIFEST + ".tmp", "w") as fh:
+        json.dump({"library": os.path.basename(LIB), "sources_sha256": source_digest(), "arch": ARCH,
+                   "units": len(UNITS), "recompiled_units": len(jobs), "forced": bool(force),
+                   "hipcc": hipcc[0] if hipcc else "", "lib_sha256": _file_sha(LIB)}, fh, indent=1)
+    os.replace(MANIFEST + ".tmp", MANIFEST)
     return LIB
+
+
+def _file_sha(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def provenance() -> dict:
+    """Whether the library on disk is the one built from this tree: the
+    manifest's source digest against the tree's, and its library hash
+    against the file."""
+    m = manifest()
+    ok_src = m.get("sources_sha256") == source_digest()
+    ok_lib = os.path.exists(LIB) and m.get("lib_sha256") == _file_sha(LIB)
+    return {"sources_match": ok_src, "library_match": ok_lib, "sources_sha256": m.get("sources_sha256", ""),
+            "recompiled_units": m.get("recompiled_units"), "hipcc": m.get("hipcc", "")}
 
 
 if __name__ == "__main__":
