@@ -9,13 +9,13 @@ V=${2:-varlibs/pw.so}
 OUT=$R/gpurun_out/raw_ab_$TAG
 mkdir -p $OUT
 cd $R
-TDBG_LIB=$V timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_stream_small.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 \
+TDBG_LIB=$V timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_stream.py tests/test_gpu_stream_small.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 120 \
   --timeout-method thread > $OUT/pytest_variant.log 2>&1 || { echo "variant parity failed"; tail -30 $OUT/pytest_variant.log; exit 11; }
 tail -1 $OUT/pytest_variant.log
 for rep in 1 2; do
   for lib in base var; do
     if [ $lib = var ]; then export TDBG_LIB=$V; else unset TDBG_LIB; fi
-    timeout -k 10 180 python -u bench.py --steps 20 --warmup 3 --variants ${VARS:-rand,ramp} --no-others --no-e2e --no-forward \
+    timeout -k 10 180 python -u bench.py --config ${CONFIG:-c5} --steps 20 --warmup 3 --variants ${VARS:-rand,ramp} --no-others --no-e2e --no-forward \
       --no-cpu-baseline --shard-tiles 0 > $OUT/${lib}_$rep.json 2> $OUT/${lib}_$rep.err \
       || { echo "bench $lib failed"; tail -20 $OUT/${lib}_$rep.err; exit 12; }
     python -c "
