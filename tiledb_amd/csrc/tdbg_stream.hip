@@ -65,6 +65,9 @@ constexpr uint32_t CCAP = sc::CODED_CAP;  // tile image bytes staged in LDS (16-
 constexpr uint32_t CPAD = 64;        // decode reads past the last window stay inside C
 constexpr uint32_t WSD = 1024;       // scratch dwords per wave (256 16-B units)
 constexpr uint32_t TABN = 256;       // BWR windows per chunk
+#ifndef TDBG_STREAM_RD128
+#define TDBG_STREAM_RD128 0  // experiment: 16-B scratch reads for the DD code realignment
+#endif
 
 struct Lds {
   uint32_t C[(CCAP + CPAD) / 4];
@@ -257,12 +260,34 @@ __device__ __forceinline__ void dd_codes_at(const uint32_t* wsp, uint32_t g, uin
   // profiles/r04/ab2_*.json -- misaligned LDS reads are slow on gfx950)
   uint32_t H[18];
   uint32_t G[20];
+#if TDBG_STREAM_RD128
+  // (experiment: six 16-B reads from g rounded down to 4 dwords, then a
+  // 2-dword select -- lanes g ~ cb/2 dwords apart make the 8-B reads 2-4-way
+  // bank conflicts; g is even, so g - g4 is 0 or 2)
+  {
+    const uint32_t g4 = g & ~3u;
+    uint32_t sm = 0u - ((g >> 1) & 1u);
+    asm volatile("" : "+v"(sm));
+    uint32_t G4[24];
+#pragma unroll
+    for (int x = 0; x < 6; x++) {
+      const v4u v = *(const v4u*)(wsp + g4 + 4 * x);
+      G4[4 * x] = v.x;
+      G4[4 * x + 1] = v.y;
+      G4[4 * x + 2] = v.z;
+      G4[4 * x + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 20; k++) G[k] = (sm & G4[k + 2]) | (~sm & G4[k]);
+  }
+#else
 #pragma unroll
   for (int x = 0; x < 10; x++) {
     const uint2 v = *(const uint2*)(wsp + g + 2 * x);
     G[2 * x] = v.x;
     G[2 * x + 1] = v.y;
   }
+#endif
 #pragma unroll
   for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
   dd_codes<CB>(H, p, n, first, x0, x1, xl, A, B);
