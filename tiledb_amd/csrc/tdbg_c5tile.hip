@@ -1,0 +1,470 @@
+// tdbg_c5tile.hip -- one-workgroup-per-tile unfilter kernel for the headline
+// pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte
+// integers, one 64 KiB chunk, DoubleDelta stored raw (dd_compressor.cc:
+// 233-236 on write, :327-331 on read): SURVEY 8(d)'s C5 "rand" and "ramp"
+// tiles, whose filtered images (40-68 KB) are above the coded kernel's
+// staging cap (tdbg_stream.hip).
+//
+// Shape (round 5, tools/ceiling3.hip, profiles/r05/): on MI355X a tile moved
+// by ONE non-persistent 1024-thread workgroup, with the launch's workgroups
+// dealt so that each XCD owns one contiguous eighth of the tiles, streams at
+// 0.77 of 8 TB/s on C5-rand-shaped tiles (68 KB in, 64 KiB out), where every
+// persistent grid of the same tiles stays at 0.64-0.68 (a wave's loads of
+// tile n + 1 wait behind its stores of tile n: gfx950 has one in-order vmcnt
+// for both).  So:
+//
+//   * grid = the launch's work items (rounded up to 8); workgroup b takes
+//     item (b & 7) * ceil(n / 8) + (b >> 3) (workgroups are dealt over the 8
+//     XCDs round-robin: this keeps each XCD on a contiguous range; a
+//     placement assumption for speed only, every item is taken exactly once
+//     whatever the placement).  Bigger launches than the grid cap loop.
+//   * The whole filtered image (<= 68,080 B at any alignment) lands in LDS
+//     by LDS-DMA (1 KiB per wave instruction, five per wave); one wave
+//     parses the tile + chunk header, every BWR window header
+//     (bit_width_reduction_filter.cc:353-380: the window table is a DPP scan
+//     of the compressed sizes), the compression frame (compression_filter.cc:
+//     413-486) and the two DD headers (dd_compressor.cc:314-331).
+//   * Ownership follows the output: thread T makes output units
+//     1024 r + T (r = 0..3; 16 B each, lane-consecutive, so every store
+//     instruction writes 1 KiB of whole lines).  Unit j is byteshuffle^-1
+//     (byteshuffle_filter.cc:111-166) of dword j of the four byte planes, i.e.
+//     of the BWR-output dwords at bytes 26 + 16384 k + 4 j (c0 = 17 B and
+//     c1's 9-byte header precede the raw values).  Each wave decodes its
+//     256-B plane ranges with one wave-uniform BWR^-1 decoder: all-raw
+//     windows (an unaligned dword read), all-8-bit windows (two bytes plus
+//     their window minima), or per element (16-bit or mixed windows).
+//
+// Tiles it does not decode (other sizes, windows not a power of two in
+// [256, 4096], a coded DD part, malformed headers, offsets tiles, images
+// over the stage) are queued for the fused kernel, which runs on the queue
+// in the same launch (and from there the general interpreter), so every
+// status and byte stays the reference's.  Nothing is written to a tile's
+// output before all its checks passed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "../../include/tiledb_amd.h"
+#include "tdbg_desc.h"
+#include "tdbg_device.h"
+#include "tdbg_launch.h"
+#include "tdbg_stream_common.h"
+
+namespace tdbg {
+namespace c5t {
+
+using namespace sc;
+
+constexpr int NT = 1024;              // 16 waves
+constexpr uint32_t OUTB = 65536;      // output bytes per tile
+constexpr uint32_t SMALL = CODED_CAP; // tiles this big or smaller belong to tdbg_stream.hip
+constexpr uint32_t IMGU = 4256;       // 16-B units of the image stage (68,096 B)
+constexpr uint32_t IMG_CAP = IMGU * 16 - 15;
+constexpr uint32_t TABN = 320;        // BWR windows per chunk (nwin <= 257 for windows >= 256 B)
+constexpr uint32_t LBWR = 65562;      // BWR output bytes of a raw-DD C5 chunk: 17 + 9 + 65536
+constexpr uint32_t OFFM = (1u << 20) - 1;
+constexpr uint32_t GRID_CAP = 1u << 22;
+
+struct Lds {
+  uint32_t IMG[IMGU * 4];
+  uint2 TAB[TABN];  // {image offset of the window's data | kind << 20, window minimum}
+  uint32_t hd[4];   // verdict, log2(window bytes), nwin - 1
+};
+
+// bytes [o, o + 4) of a dword array (any alignment)
+__device__ __forceinline__ uint32_t rd32(const uint32_t* a, uint32_t o) {
+  return __builtin_amdgcn_alignbyte(a[(o >> 2) + 1], a[o >> 2], o & 3);
+}
+
+template <bool SGN>
+__device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
+  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
+}
+
+// the tile's shape is one this kernel decodes (descriptor checks only)
+__device__ __forceinline__ bool takes(const KParams& kp, const Desc& d) {
+  return !(kp.flags & TDBG_TILE_OFFSETS) && d.os == OUTB && (((uintptr_t)d.out) & 15) == 0 &&
+         d.fs <= IMG_CAP;
+}
+
+__device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
+  if (threadIdx.x == 0) {
+    const uint32_t k = atomicAdd(kp.sq, 1u);
+    if (k < kp.sq_cap) kp.sq[1 + k] = (uint32_t)t;
+    else if (kp.status) kp.status[kp.chunks ? kp.chunks[t].tile : t] = TDBG_E_INTERNAL;
+  }
+}
+
+// work item t's descriptor (every lane reads the same item)
+__device__ __forceinline__ Desc load_desc(const KParams& kp, uint64_t t) {
+  Desc d;
+  d.t = t;
+  if (kp.chunks) {
+    const ChunkRec r = kp.chunks[t];
+    const uint64_t fs = 12ull + r.ml + r.fl;
+    d.fs = fs;
+    d.os = r.orig;
+    d.in = kp.in[r.tile] + r.in_off - 12;
+    d.out = kp.out[r.tile] + r.out_off;
+  } else {
+    d.fs = kp.in_size[t];
+    d.os = kp.out_size[t];
+    d.in = kp.in[t];
+    d.out = kp.out[t];
+  }
+  return d;
+}
+
+// ---------------------------------------------------------------------------
+// header parse (one wave): tile/chunk header, window table, frame, DD headers
+// ---------------------------------------------------------------------------
+template <bool SGN>
+__device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool chunked) {
+  const uint32_t* P = L.IMG;
+  // the chunk header follows the tile's u64 chunk count, or (chunk mode: a
+  // chunk of a multi-chunk tile) starts the image
+  const uint32_t ho = chunked ? 0u : 8u;
+  const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
+  const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + ho), fl = rd32(P, b + ho + 4),
+                 ml = rd32(P, b + ho + 8);
+  const uint32_t m = b + ho + 12;
+  const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4);
+  bool ok = (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= d.fs && nwr >= 2 &&
+            nwr <= TABN && ml == 8 + 9 * nwr + 24 && Lb == LBWR;
+  const uint32_t nwin = ok ? nwr : 2;
+  // lane l: windows 5l..5l+4 = 45 bytes at e0 (m + 8 + 45 * 63 + 48 < 4096);
+  // window q's header: [T min][u8 bits][u32 bytes] at e0 + 9 q.  Two passes
+  // (sizes and checks; then, after the scan, the table entries) so that few
+  // values stay live (the kernel runs at 64 VGPRs).
+  const uint32_t e0 = m + 8 + 45 * l;
+  const uint32_t ws = __builtin_amdgcn_readfirstlane(rd32(P, m + 8 + 5));  // window 0's byte count
+  ok = ok && ws >= 256 && ws <= 4096 && (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwin;
+  auto win = [&](uint32_t q, uint32_t& kind, uint32_t& cs, uint32_t& mn, bool& bad) {
+    const uint32_t wi = 5 * l + q;
+    const uint32_t vmin = rd32(P, e0 + 9 * q), bits = rd32(P, e0 + 9 * q + 4) & 0xffu, nb = rd32(P, e0 + 9 * q + 5);
+    const bool in = wi < nwin;
+    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+    bad = (in && nb != want);
+    const bool raw = bits >= 32 || (nb & 3) != 0;
+    bad = bad || (in && !raw && bits != 8 && bits != 16);
+    kind = raw ? 2 : bits == 8 ? 0 : 1;
+    cs = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+    mn = raw ? 0 : vmin;
+  };
+  uint32_t s5 = 0;
+  bool bad = false;
+#pragma unroll
+  for (uint32_t q = 0; q < 5; q++) {
+    uint32_t kd, c, mv;
+    bool bq;
+    win(q, kd, c, mv, bq);
+    s5 += c;
+    bad = bad || bq;
+  }
+  const uint32_t inc = wave_incscan_u32(s5);
+  ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
+  const uint32_t dst = ho + 12 + ml;  // image offset of the BWR data
+  {
+    uint32_t off = dst + inc - s5;
+#pragma unroll
+    for (uint32_t q = 0; q < 5; q++) {
+      uint32_t kd, c, mv;
+      bool bq;
+      win(q, kd, c, mv, bq);
+      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kd << 20), mv);
+      off += c;
+    }
+  }
+  // compression frame md (compression_filter.cc:413-486): 1 md part of 8 B
+  // (the byteshuffle header) compressed to 17 B, 1 data part of 65,536 B
+  // compressed to 9 + 65,536 B (raw DoubleDelta)
+  const uint32_t f = m + 8 + 9 * nwin;
+  ok = ok && rd32(P, f) == 1 && rd32(P, f + 4) == 1 && rd32(P, f + 8) == 8 && rd32(P, f + 12) == 17 &&
+       rd32(P, f + 16) == OUTB && rd32(P, f + 20) == 9 + OUTB;
+  // DD headers = BWR-output bytes [0, 26): elements 0..6 of window 0 (lane e
+  // decodes element e)
+  uint32_t k0, mn0;
+  {
+    uint32_t c;
+    bool bq;
+    win(0, k0, c, mn0, bq);
+    k0 = __builtin_amdgcn_readfirstlane(k0);
+    mn0 = __builtin_amdgcn_readfirstlane(mn0);
+  }
+  const uint32_t e = l < 7 ? l : 6;
+  uint32_t v;
+  if (k0 == 2) v = rd32(P, b + dst + 4 * e);
+  else if (k0 == 0) v = ext<SGN>(rd32(P, b + dst + e), 0, 8) + mn0;
+  else v = ext<SGN>(rd32(P, b + dst + 2 * e), 0, 16) + mn0;
+  auto dw = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(v, k); };
+  auto at = [&](int o) -> uint32_t { return __builtin_amdgcn_alignbyte(dw((o >> 2) + 1), dw(o >> 2), o & 3); };
+  // c0 = [u8 bitsize][u64 n = 2][1][65536] (any bitsize: two values, or the
+  // same 8 bytes copied raw); c1 = [u8 bitsize >= 31][u64 16384] + raw values
+  ok = ok && at(1) == 2 && at(5) == 0 && at(9) == 1 && at(13) == OUTB && (at(17) & 0xffu) >= 31 &&
+       at(18) == OUTB / 4 && at(22) == 0;
+  if (l == 0) {
+    L.hd[0] = ok ? 1u : 0u;
+    L.hd[1] = 31 - __builtin_clz(ws);
+    L.hd[2] = nwin - 1;
+  }
+}
+
+// Byteshuffle^-1 of one output unit from dword j of the four planes: out
+// dword b, byte k = plane k's byte b
+__device__ __forceinline__ v4u unshuffle4(const uint32_t (&x)[4]) {
+  const uint32_t t0 = __builtin_amdgcn_perm(x[1], x[0], 0x05010400u);
+  const uint32_t t1 = __builtin_amdgcn_perm(x[1], x[0], 0x07030602u);
+  const uint32_t t2 = __builtin_amdgcn_perm(x[3], x[2], 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(x[3], x[2], 0x07030602u);
+  return v4u{__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
+             __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
+}
+
+// The wave's plane ranges: (r, k) = round r (output units 1024 r + 64 w +
+// [0, 64)), plane k = the 256 BWR-output bytes [Q0, Q0 + 256), Q0 = 26 +
+// 16384 k + 4 (1024 r + 64 w).  A range spans at most two windows (windows
+// are >= 256 B), W0 and W1; lane i < 16 reads range i = 4 r + k's two table
+// entries once, and the decode takes them back with v_readlane (no per-lane
+// table lookups).  One wave-uniform BWR^-1 decoder per range:
+//   raw     both windows raw: the compressed dword at W0's data offset +
+//           (Q - W0's start) (consecutive full raw windows are contiguous);
+//   8-bit   both 8-bit: the two element bytes at W0's offset + element index
+//           (full 8-bit windows are contiguous too), each plus its window's
+//           minimum;
+//   general (16-bit or mixed windows) the dword = upper half of element e =
+//           Q / 4 and lower half of e + 1 (Q = 2 mod 4), each decoded from
+//           its own window's entry.
+struct Ranges {
+  uint32_t x0, x1;  // table words of W0 and W1 ({data offset | kind << 20})
+  uint32_t m0, m1;  // their minima
+  uint32_t e0, e1;  // their first element indices (e1 = W1's, or ~0 when W1 == W0)
+  uint32_t s1;      // the decoded value of element e1 (W1's first element)
+  uint32_t base;    // raw / 8-bit ranges: LDS byte of the range's first compressed dword / element byte
+  uint32_t is8, gen;  // 16-bit masks over ranges 4 r + k
+};
+
+template <bool SGN>
+__device__ __forceinline__ Ranges setup_ranges(const Lds& L, uint32_t b, uint32_t w, uint32_t l, uint32_t wsh) {
+  const uint32_t esh = wsh - 2;
+  const uint32_t i = l & 15, r = i >> 2, k = i & 3;
+  const uint32_t Q0 = 26 + 16384 * k + 4 * (1024 * r + 64 * w);
+  const uint32_t W0 = Q0 >> wsh, W1 = (Q0 + 255) >> wsh;
+  const uint2 t0 = L.TAB[W0], t1 = L.TAB[W1];
+  const uint32_t k0 = t0.x >> 20, k1 = t1.x >> 20;
+  const bool raw = k0 == 2 && k1 == 2, b8 = k0 == 0 && k1 == 0;
+  Ranges g;
+  g.x0 = t0.x;
+  g.x1 = t1.x;
+  g.m0 = t0.y;
+  g.m1 = t1.y;
+  g.e0 = W0 << esh;
+  g.e1 = W1 > W0 ? W1 << esh : 0xffffffffu;
+  {
+    const uint32_t y = rd32(L.IMG, (t1.x & OFFM) + b);
+    g.s1 = k1 == 2 ? y : (k1 == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + t1.y;
+  }
+  g.base = raw ? (t0.x & OFFM) + (Q0 - (W0 << wsh)) + b : (t0.x & OFFM) + ((Q0 >> 2) - (W0 << esh)) + b;
+  g.is8 = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && b8);
+  g.gen = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && !raw && !b8);
+  return g;
+}
+
+// General ranges (16-bit windows, or two windows of different kinds): lane
+// l's dword = the upper half of element e and the lower half of e + 1.  Both
+// come from one read at element e's compressed value in its own window (W0's
+// below e1, else W1's; raw: from its byte 2, so the read holds exactly the
+// dword), except for the one lane whose e + 1 is W1's first element: that
+// half is the range's s1.  The v_readlane's are taken before any select (a
+// readlane under a lane-dependent condition becomes an exec-masked branch).
+struct GenRange {
+  uint32_t x0, x1, m0, m1, e0, e1, s1;
+};
+__device__ __forceinline__ GenRange gen_range(const Ranges& g, uint32_t i) {
+  return GenRange{(uint32_t)__builtin_amdgcn_readlane(g.x0, i), (uint32_t)__builtin_amdgcn_readlane(g.x1, i),
+                  (uint32_t)__builtin_amdgcn_readlane(g.m0, i), (uint32_t)__builtin_amdgcn_readlane(g.m1, i),
+                  (uint32_t)__builtin_amdgcn_readlane(g.e0, i), (uint32_t)__builtin_amdgcn_readlane(g.e1, i),
+                  (uint32_t)__builtin_amdgcn_readlane(g.s1, i)};
+}
+__device__ __forceinline__ uint32_t gen_addr(const GenRange& q, uint32_t e, uint32_t b) {
+  const bool hi = e >= q.e1;
+  const uint32_t tx = hi ? q.x1 : q.x0, st = hi ? q.e1 : q.e0, kind = tx >> 20;
+  return (tx & OFFM) + ((e - st) << kind) + b + (kind == 2 ? 2u : 0u);
+}
+template <bool SGN>
+__device__ __forceinline__ uint32_t gen_dword(const GenRange& q, uint32_t e, uint32_t y) {
+  const bool hi = e >= q.e1;
+  const uint32_t tx = hi ? q.x1 : q.x0, mn = hi ? q.m1 : q.m0, kind = tx >> 20;
+  const uint32_t v0 = (kind == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + mn;
+  const uint32_t v1 = (kind == 0 ? ext<SGN>(y, 8, 8) : ext<SGN>(y, 16, 16)) + mn;
+  const uint32_t a = kind == 2 ? y : v0 >> 16;
+  const uint32_t bn = kind == 2 ? y >> 16 : v1;
+  const uint32_t bh = e + 1 == q.e1 ? q.s1 : bn;
+  return __builtin_amdgcn_perm(bh, a, 0x05040100u);
+}
+
+// NR ranges (NR / 4 rounds from round r0): reads, decode, stores
+template <bool SGN, int ABL, bool GEN, int NR>
+__device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint32_t b, uint32_t w, uint32_t l,
+                                             uint8_t* o, uint32_t r0) {
+  uint32_t y[NR];
+#pragma unroll
+  for (uint32_t j = 0; j < NR; j++) {
+    const uint32_t i = 4 * r0 + j;
+    const uint32_t e = ((26 + 16384 * (i & 3) + 4 * (1024 * (i >> 2) + 64 * w)) >> 2) + l;
+    uint32_t a = __builtin_amdgcn_readlane(g.base, i) + (((g.is8 >> i) & 1) ? l : 4 * l);
+    if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b);
+    y[j] = (ABL == 1 || ABL == 2) ? l + i : rd32(L.IMG, a);
+  }
+#pragma unroll
+  for (uint32_t rr = 0; rr < NR / 4; rr++) {
+    const uint32_t r = r0 + rr;
+    uint32_t x[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t i = 4 * r + k;
+      x[k] = y[4 * rr + k];
+      if (ABL == 1 || ABL == 2 || ABL == 5) continue;
+      const uint32_t e = ((26 + 16384 * k + 4 * (1024 * r + 64 * w)) >> 2) + l;
+      // (wave-uniform branches: all 16 reads are already in flight)
+      if ((g.is8 >> i) & 1) {
+        const uint32_t m0 = __builtin_amdgcn_readlane(g.m0, i), m1 = __builtin_amdgcn_readlane(g.m1, i),
+                       e1 = __builtin_amdgcn_readlane(g.e1, i);
+        const uint32_t v0 = ext<SGN>(x[k], 0, 8) + (e < e1 ? m0 : m1), v1 = ext<SGN>(x[k], 8, 8) + (e + 1 < e1 ? m0 : m1);
+        x[k] = __builtin_amdgcn_perm(v1, v0, 0x05040302u);
+      } else if (GEN && ((g.gen >> i) & 1)) {
+        x[k] = gen_dword<SGN>(gen_range(g, i), e, x[k]);
+      }
+    }
+    const v4u v = unshuffle4(x);
+    if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
+      __builtin_nontemporal_store(v, (g_u4*)(o + 16384u * r));
+  }
+}
+
+// ABL (timing ablations, outputs not meaningful): 1 no parse and no decode
+// (DMA, barriers, constant stores), 2 parse but no decode, 3 no stores,
+// 4 every wave on the one-read path, 5 no 8-bit combine
+template <bool SGN, int ABL>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
+  __shared__ Lds L;
+  const uint32_t w = wave_(), l = lane_();
+  // diagnostics (KParams::prof, TDBG_PROF=1): shader clocks of workgroups
+  // < 1024 (slots 8.. of the profile buffer's rows; the fused kernel, which runs
+  // next, writes 0..7): 0 DMA wait, 1 parse, 2 range setup,
+  // 3 / 4 / 5 decode + stores of waves 0 / 1 / 15, 6 whole workgroup
+  uint64_t* const prof = kp.prof && blockIdx.x < 1024 ? kp.prof + (uint64_t)blockIdx.x * TDBG_PROF_PHASES + 8 : nullptr;
+  const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  // this workgroup's work item: the XCD-contiguous deal of [base, base + cnt)
+  const uint32_t n8 = (cnt + 7) >> 3;
+  const uint32_t j = (blockIdx.x & 7) * n8 + (blockIdx.x >> 3);
+  if (j >= cnt) return;
+  const uint64_t t = (uint64_t)base + j;
+  if (t >= work_items(kp)) return;
+  const bool chunked = kp.chunks != nullptr;
+  const Desc d = load_desc(kp, t);
+  if (d.fs <= SMALL) return;  // the coded kernel's class
+  if (!takes(kp, d)) {
+    decline(kp, t);
+    return;
+  }
+  // the image's aligned cover: every wave moves units 64 (w + 16 i) + l
+  {
+    const uint64_t a0 = (uint64_t)d.in & ~15ull;
+    const uint32_t nu = (uint32_t)((((uint64_t)d.in & 15) + d.fs + 15) >> 4);
+#pragma unroll
+    for (uint32_t i = 0; i < (IMGU + NT - 1) / NT; i++) {
+      const uint32_t u0 = 64 * (w + 16 * i);
+      if (u0 < nu && u0 + l < nu) dma16(a0 + 16ull * (u0 + l), lds_addr(L.IMG) + 16 * u0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  const uint64_t c1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  if (w == 0 && ABL != 1) parse<SGN>(L, d, l, chunked);
+  lds_barrier();
+  const uint64_t c2 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
+    decline(kp, t);
+    return;
+  }
+  const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
+  const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
+  const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh);
+  uint8_t* const o = d.out + 16u * (64 * w + l);
+  const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
+  // All 16 ranges' reads first, then the decode and one store per round.
+  // Raw and 8-bit ranges read one dword (the decoder picked by a select).
+  // The few general ranges (a wave of a ramp tile on a plane boundary) take
+  // the per-element decoder under a wave-uniform branch that holds no LDS
+  // access, so the reads stay in flight together (8 at a time in such waves,
+  // for registers).
+  if (g.gen == 0 || ABL == 4) {
+    decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0);
+  } else if (ABL == 6) {
+    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0);
+    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2);
+  } else {
+    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0);
+    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2);
+  }
+  if (prof && l == 0) {
+    const uint64_t c4 = __builtin_amdgcn_s_memtime();
+    if (w == 0) {
+      prof[0] = c1 - c0;
+      prof[1] = c2 - c1;
+      prof[2] = c3 - c2;
+      prof[3] = c4 - c3;
+      prof[6] = c4 - c0;
+    }
+    if (w == 1) prof[4] = c4 - c3;
+    if (w == 15) prof[5] = c4 - c3;
+  }
+  if (threadIdx.x == 0) {
+    if (kp.status && !chunked) kp.status[t] = TDBG_OK;
+    if (kp.stats) {
+      // one slot of 16 counters per 64 workgroups (tdbg_host.cpp read_stats
+      // sums the slots): one address for every workgroup of a 100,000-tile
+      // launch would serialise its atomics
+      uint64_t* s = kp.stats + TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63));
+      if (chunked) {
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_CHUNKS], 1ull);
+      } else {
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_RAW_TILES], 1ull);
+      }
+    }
+  }
+}
+
+}  // namespace c5t
+}  // namespace tdbg
+
+// one workgroup per work item (kp->ntiles of them, or in chunk mode the
+// directory's capacity: items past the device count exit at once); launches
+// of at most GRID_CAP items
+extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s) {
+  using namespace tdbg::c5t;
+  static const int abl = getenv("TDBG_C5T_ABL") ? atoi(getenv("TDBG_C5T_ABL")) : 0;  // experiments
+  auto k = sgn ? (abl == 1   ? unfilter_c5tile_kernel<true, 1>
+                  : abl == 2 ? unfilter_c5tile_kernel<true, 2>
+                  : abl == 3 ? unfilter_c5tile_kernel<true, 3>
+                  : abl == 4 ? unfilter_c5tile_kernel<true, 4>
+                  : abl == 5 ? unfilter_c5tile_kernel<true, 5>
+                  : abl == 6 ? unfilter_c5tile_kernel<true, 6>
+                             : unfilter_c5tile_kernel<true, 0>)
+               : unfilter_c5tile_kernel<false, 0>;
+  for (uint64_t base = 0; base < kp->ntiles; base += GRID_CAP) {
+    const uint32_t cnt = (uint32_t)std::min<uint64_t>(kp->ntiles - base, GRID_CAP);
+    const uint32_t grid = 8 * ((cnt + 7) / 8);
+    TDBG_LAUNCH(k, dim3(grid), dim3(NT), s, *kp, (uint32_t)base, cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}

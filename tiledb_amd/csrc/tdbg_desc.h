@@ -62,6 +62,14 @@ enum tdbg_stat_slot : uint32_t {
   TDBG_STAT_STREAM_CHUNKS = 8,  // chunk-parallel launches: chunks the streaming kernels took
   TDBG_STAT_N = 9
 };
+// The counters live in slots of TDBG_STAT_STRIDE u64 (one 128-B line each):
+// slot 0 takes the persistent kernels' one add per workgroup, slots 1..64 the
+// one-workgroup-per-tile kernels' (workgroup b adds to slot 1 + (b & 63), so
+// a 100,000-workgroup launch spreads its atomics over 64 lines); the host
+// sums the slots (tdbg_host.cpp read_stats).
+#define TDBG_STAT_STRIDE 16
+#define TDBG_STAT_SLOTS 65
+static_assert(TDBG_STAT_N <= TDBG_STAT_STRIDE, "stat slot");
 
 // host-side internals shared by tdbg_host.cpp and tdbg_cpu.cpp
 struct tdbg_pipeline;

@@ -64,6 +64,7 @@ extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid,
 extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
+extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                hipStream_t s);
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
@@ -563,8 +564,8 @@ int tdbg_context_create(int device, tdbg_context** out) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
     c->cus = cus;
-  hipError_t e = hipMalloc(&c->d_stats, sizeof(uint64_t) * TDBG_STAT_N);
-  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, sizeof(uint64_t) * TDBG_STAT_N);
+  hipError_t e = hipMalloc(&c->d_stats, sizeof(uint64_t) * TDBG_STAT_STRIDE * TDBG_STAT_SLOTS);
+  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, sizeof(uint64_t) * TDBG_STAT_STRIDE * TDBG_STAT_SLOTS);
   if (e != hipSuccess) {
     if (c->d_stats) (void)hipFree(c->d_stats);
     delete c;
@@ -690,6 +691,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
   static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
+  static const bool c5_old_raw = getenv("TDBG_C5_OLD_RAW") != nullptr;  // A/B: the persistent raw-DD kernel
   const bool c5_stream = (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
                          p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
   // The scan pipelines of C3a / C3b / C4 on 8-byte values first go through
@@ -805,7 +807,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
       if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
-      if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      if (!skip_fused) e = c5_old_raw ? tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream)
+                                      : tdbg_launch_c5tile(&ks, sgn, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
     tdbg::KParams kf = kp;  // the fused kernel on the chunks they queued
@@ -832,7 +835,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
       if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
-      if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      if (!skip_fused) e = c5_old_raw ? tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream)
+                                      : tdbg_launch_c5tile(&ks, sgn, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
     tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
@@ -979,8 +983,13 @@ int tdbg_unfilter_tiles_sync(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
 static int read_stats(const tdbg_context* c, uint64_t (&h)[TDBG_STAT_N]) {
   HIP_OK(hipSetDevice(c->device));
   const hipStream_t s = c->last_stream_set ? c->last_stream : nullptr;
-  HIP_OK(hipMemcpyAsync(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+  uint64_t all[TDBG_STAT_STRIDE * TDBG_STAT_SLOTS];
+  HIP_OK(hipMemcpyAsync(all, c->d_stats, sizeof(all), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  for (int i = 0; i < TDBG_STAT_N; i++) {
+    h[i] = 0;
+    for (int k = 0; k < TDBG_STAT_SLOTS; k++) h[i] += all[TDBG_STAT_STRIDE * k + i];
+  }
   return TDBG_OK;
 }
 
