@@ -168,8 +168,14 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
     fused1, fb1, _ = ctx.path_stats()
     s1 = ctx.stream_tiles()
     c1 = ctx.stream_chunks()
+    batch.d_status.fill_(-1)
     ev_elapsed = timed(True)
     kern_ms, total_ms = ctx.launch_times(steps)
+    # (the event-bound pass, whose kernel times `roofline` reports, is checked
+    # the same way)
+    st = batch.d_status[: batch.ntiles].cpu().numpy()
+    if st.any():
+        raise SystemExit(f"event-timed launches: device status nonzero: {np.unique(st)}")
     if dist is not None:
         elapsed = max_over_ranks(dist, elapsed, DIST_DEV)
         ev_elapsed = max_over_ranks(dist, ev_elapsed, DIST_DEV)

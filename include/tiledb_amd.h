@@ -469,7 +469,11 @@ int tdbg_dense_read_host(tdbg_context* ctx, const tdbg_pipeline* p, uint64_t nti
  * Where domains overlap, the fragment with the LOWER index wins (the
  * reference walks them from the last to the first, each overwriting); cells
  * no fragment covers get the fill value (Attribute::fill_value) and
- * fill_validity.  Result buffers are in the query layout (base.layout). */
+ * fill_validity, and so do cells of the subarray in no given space tile (the
+ * async entries write the fill value into every result cell first).  A
+ * present fragment without a validity tile (d_validity NULL, or its entry
+ * NULL) counts as valid.  Result buffers are in the query layout
+ * (base.layout). */
 typedef struct tdbg_dense_frag_config {
   tdbg_dense_copy_config base; /* dims, subarray, tile extents, cell/result order;
                                   base.cell_size: bytes per cell (fixed), 8 (var) */
@@ -493,7 +497,10 @@ int tdbg_dense_copy_fragments_async(tdbg_context* ctx, const tdbg_dense_frag_con
  * unfiltered offsets tiles (uint64, tile cells + 1 entries: the extra offset
  * of tile.h:144-146 included) and var tiles, the result offsets (uint64, one
  * per result cell, in elements in elements mode) and their total
- * (*d_var_total, device); the cells' source addresses stay in ctx for step 2. */
+ * (*d_var_total, device); the cells' source addresses stay in ctx for step 2.
+ * A cell whose offsets o[i] <= o[i + 1] <= o[tile cells] do not hold is
+ * read as empty (nothing is read outside a var tile) and flags the context;
+ * tdbg_dense_read_var_host returns TDBG_E_DATA_READ for it. */
 int tdbg_dense_var_offsets_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
                                  const int64_t* d_tile_start, const int64_t* d_frag_dom,
                                  const uint8_t* const* d_offset_tiles, const uint8_t* const* d_var_tiles,
@@ -515,7 +522,11 @@ int tdbg_dense_var_copy_async(tdbg_context* ctx, const tdbg_dense_frag_config* c
  * *var_total receives the var bytes; TDBG_E_OUT_FULL if var_cap is smaller
  * (nothing copied to result_var).  Statuses per (tile, fragment) pair: the
  * offsets tile's, or the var tile's if that one failed.  cfg->nullable must
- * be 0 here (validity tiles: tdbg_dense_var_offsets_async). */
+ * be 0 here (validity tiles: tdbg_dense_var_offsets_async).  The space tiles
+ * must cover the subarray exactly once on one tile grid (TDBG_E_ARG
+ * otherwise), as the reference iterates every space tile of the subarray;
+ * tiles whose stages outgrow the default scratch are redone through the
+ * sync entry's retry, as in tdbg_unfilter_tiles_sync. */
 int tdbg_dense_read_var_host(tdbg_context* ctx, const tdbg_pipeline* p_offsets, const tdbg_pipeline* p_var,
                              const tdbg_dense_frag_config* cfg, uint64_t ntiles, const int64_t* tile_start,
                              const int64_t* frag_dom, const uint8_t* const* off_filtered,

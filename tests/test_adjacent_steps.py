@@ -134,14 +134,45 @@ def test_read_unfilter_tiles_from_files(oracle_mod, cfg_kind):
 
 
 @pytest.mark.gpu
-def test_read_unfilter_statuses_after_device_failure(oracle_mod, monkeypatch):
+def test_read_unfilter_statuses_after_device_failure():
     """A device error in block 1 (injected: TDBG_DEBUG_IO_FAIL_BLOCK) after a
     block holding a corrupt tile: block 0 keeps its real statuses (the corrupt
     tile's error, OK for the rest), every tile of block 1 and after says
     TDBG_E_NOT_RUN -- never OK for output that was not written -- and the call
-    raises the device error although some tiles carry statuses."""
+    raises the device error although some tiles carry statuses.  The fault
+    injection exists only in the experiments library (tdbg_hooks.h), so the
+    case runs in a child process that loads it (TDBG_LIB)."""
+    import subprocess
+    import sys
+    from tiledb_amd import build as B
+    assert os.path.exists(B.EXP_LIB), "experiments library missing: __graft_entry__.build() builds it"
+    env = dict(os.environ, TDBG_LIB=os.path.basename(B.EXP_LIB))
+    code = ("import sys; sys.path.insert(0, %r); from oracle import oracle as O; O.build(); "
+            "from tests.test_adjacent_steps import _device_failure_case; _device_failure_case(O)" % B.ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_product_library_ignores_hooks():
+    """The product library reads no TDBG_* timing, ablation or fault hook
+    (tdbg_hooks.h compiles them out): none of their names is left in it,
+    while the experiments library keeps them."""
+    from tiledb_amd import build as B
+    names = (b"TDBG_DEBUG_STOP", b"TDBG_NO_STREAM", b"TDBG_DEBUG_SKIP_FUSED", b"TDBG_DEBUG_SKIP_FIXUP",
+             b"TDBG_DEBUG_IO_FAIL_BLOCK", b"TDBG_C5T_ABL", b"TDBG_DEBUG_TILE_MODE", b"TDBG_C5_OLD_RAW")
+    with open(B.LIB, "rb") as fh:
+        blob = fh.read()
+    for name in names:
+        assert name not in blob, name
+    if os.path.exists(B.EXP_LIB):
+        with open(B.EXP_LIB, "rb") as fh:
+            assert b"TDBG_DEBUG_IO_FAIL_BLOCK" in fh.read()
+
+
+def _device_failure_case(oracle_mod):
     import torch
     assert torch.cuda.is_available()
+    monkeypatch = pytest.MonkeyPatch()
     from tiledb_amd import _native, engine
     tiles, vals = W.c5_pool("active", 8, seed=7)
     tiles = [bytearray(t) for t in tiles]

@@ -7,6 +7,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
+import sys
 
 try:  # torch ships its own libamdhip64; load it first so one HIP runtime is used
     import torch  # noqa: F401
@@ -15,10 +17,15 @@ except Exception:  # pragma: no cover - torch is optional for pure C-ABI use
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtiledb_amd.so")
-# experiments only: TDBG_LIB names another in-tree build of the same C-ABI
-# (e.g. the previous commit's kernels, for same-box A/B timing)
+# experiments and fault-injection tests only: TDBG_LIB names another in-tree
+# build of the same C-ABI in this package directory (the experiments library
+# libtiledb_amd_exp.so, or an earlier commit's build for same-box A/B timing)
 if os.environ.get("TDBG_LIB"):
-    LIB_PATH = os.path.join(_HERE, os.environ["TDBG_LIB"])
+    _name = os.environ["TDBG_LIB"]
+    if os.path.basename(_name) != _name or not re.fullmatch(r"libtiledb_amd[A-Za-z0-9_]*\.so", _name):
+        raise ImportError(f"TDBG_LIB={_name!r}: not a libtiledb_amd*.so in {_HERE}")
+    LIB_PATH = os.path.join(_HERE, _name)
+    sys.stderr.write(f"tiledb_amd: TDBG_LIB set, loading {LIB_PATH} instead of the product library\n")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -15,6 +15,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libtiledb_amd.so")
+# The experiments build (timing ablations, A/B switches, fault injection and
+# phase clocks read from TDBG_* environment variables, tdbg_hooks.h): the
+# units that read hooks are compiled again with -DTDBG_EXPERIMENTS, every
+# other object is shared with the product library.  Only tests that inject
+# faults (in a subprocess, through TDBG_LIB) and the tools/ studies load it.
+EXP_LIB = os.path.join(HERE, "libtiledb_amd_exp.so")
 # Build provenance: the digest of every source, header and flag the library
 # was built from, written next to it (travels with it to the GPU box, stays
 # out of git like the library).  build() rebuilds whenever the tree's digest
@@ -43,7 +49,10 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           for k in range(NPART)])
 HOST_ONLY = {"tdbg_cpu.cpp"}
 NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip", "tdbg_c5tile.hip"}  # checked with -Rpass-analysis
-HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h", "tdbg_launch.h"]
+HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h", "tdbg_launch.h",
+           "tdbg_hooks.h"]
+HOOK_UNITS = {"tdbg_host.cpp", "tdbg_io.cpp", "tdbg_c5tile.hip", "tdbg_stream.hip", "tdbg_stream_raw.hip",
+              "tdbg_stream_small.hip"}
 
 
 def _deps(src: str):
@@ -87,10 +96,16 @@ def _stale() -> bool:
     return manifest().get("sources_sha256") != source_digest()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, experiments: bool = False) -> str:
+    lib = _build(force, verbose)
+    if experiments:
+        _build_exp(force, verbose)
+    return lib
+
+
+def _build(force: bool, verbose: bool) -> str:
     if not force and not _stale():
         return LIB
-    from concurrent.futures import ThreadPoolExecutor
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}",
@@ -108,14 +123,30 @@ def build(force: bool = False, verbose: bool = False) -> str:
         cmd = [HIPCC] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         jobs.append(cmd)
 
+    _compile(jobs, verbose)
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    hipcc = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+    with open(MANIFEST + ".tmp", "w") as fh:
+        json.dump({"library": os.path.basename(LIB), "sources_sha256": source_digest(), "arch": ARCH,
+                   "units": len(UNITS), "recompiled_units": len(jobs), "forced": bool(force),
+                   "hipcc": hipcc[0] if hipcc else "", "lib_sha256": _file_sha(LIB)}, fh, indent=1)
+    os.replace(MANIFEST + ".tmp", MANIFEST)
+    return LIB
+
+
+def _compile(jobs, verbose: bool) -> None:
+    from concurrent.futures import ThreadPoolExecutor
+
     def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         src = cmd[cmd.index("-c") + 1]
         if os.path.basename(src) in NO_SCRATCH:
-            # the streaming kernels count their own vector-memory operations
-            # (s_waitcnt vmcnt(N)): a register spill would add scratch
-            # loads/stores to the count, so the build refuses any
             r = subprocess.run(cmd + ["-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
             if r.returncode:
                 sys.stderr.write(r.stderr)
@@ -130,19 +161,32 @@ def build(force: bool = False, verbose: bool = False) -> str:
     nproc = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(nproc) as ex:
         list(ex.map(run, jobs))
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    hipcc = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
-    with open(MANIFEST + ".tmp", "w") as fh:
-        json.dump({"library": os.path.basename(LIB), "sources_sha256": source_digest(), "arch": ARCH,
-                   "units": len(UNITS), "recompiled_units": len(jobs), "forced": bool(force),
-                   "hipcc": hipcc[0] if hipcc else "", "lib_sha256": _file_sha(LIB)}, fh, indent=1)
-    os.replace(MANIFEST + ".tmp", MANIFEST)
-    return LIB
+
+
+def _build_exp(force: bool, verbose: bool) -> str:
+    """libtiledb_amd_exp.so: the product objects, with the hook units
+    recompiled under -DTDBG_EXPERIMENTS (the product library is built first)."""
+    objdir = os.path.join(HERE, "build")
+    common = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}",
+              "-I", os.path.join(ROOT, "include"), "-DTDBG_EXPERIMENTS"]
+    jobs, objs = [], []
+    for src, name, extra in UNITS:
+        if src not in HOOK_UNITS:
+            objs.append(os.path.join(objdir, name + ".o"))
+            continue
+        obj = os.path.join(objdir, name + "_exp.o")
+        objs.append(obj)
+        if not force and not _newer(obj, _deps(src)):
+            continue
+        flags = (["-x", "hip"] if src.endswith(".cpp") else []) + common
+        jobs.append([HIPCC] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj])
+    if not jobs and not _newer(EXP_LIB, objs):
+        return EXP_LIB
+    _compile(jobs, verbose)
+    tmp = EXP_LIB + ".tmp"
+    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"])
+    os.replace(tmp, EXP_LIB)
+    return EXP_LIB
 
 
 def _file_sha(path: str) -> str:
@@ -165,4 +209,4 @@ def provenance() -> dict:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, experiments="--experiments" in sys.argv))

@@ -52,6 +52,7 @@
 #include "tdbg_device.h"
 #include "tdbg_launch.h"
 #include "tdbg_stream_common.h"
+#include "tdbg_hooks.h"
 
 namespace tdbg {
 namespace c5t {
@@ -71,7 +72,8 @@ constexpr uint32_t GRID_CAP = 1u << 22;
 struct Lds {
   uint32_t IMG[IMGU * 4];
   uint2 TAB[TABN];  // {image offset of the window's data | kind << 20, window minimum}
-  uint32_t hd[4];   // verdict, log2(window bytes), nwin - 1
+  uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1
+  uint32_t red[16][2];  // coded tiles: each wave's DD aggregate (A, B)
 };
 
 // bytes [o, o + 4) of a dword array (any alignment)
@@ -121,6 +123,11 @@ __device__ __forceinline__ Desc load_desc(const KParams& kp, uint64_t t) {
 // ---------------------------------------------------------------------------
 // header parse (one wave): tile/chunk header, window table, frame, DD headers
 // ---------------------------------------------------------------------------
+// Two LDS round trips: (1) the tile + chunk header and every window header
+// (lane l: windows 5 l .. 5 l + 4, 45 bytes), issued together (the window
+// headers' place does not depend on any value read); (2) after the scan of
+// the compressed sizes, the compression frame (after the nwin window
+// headers) and the DD headers (BWR-output elements 0..8, in window 0).
 template <bool SGN>
 __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool chunked) {
   const uint32_t* P = L.IMG;
@@ -128,87 +135,90 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   // chunk of a multi-chunk tile) starts the image
   const uint32_t ho = chunked ? 0u : 8u;
   const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
+  const uint32_t m = b + ho + 12;
+  const uint32_t e0 = m + 8 + 45 * l;  // m + 8 + 45 * 63 + 52 < 3,000
+  // ---- round 1
+  uint32_t R[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) R[k] = P[(e0 >> 2) + k];
+  // (uniform addresses: broadcast reads)
   const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + ho), fl = rd32(P, b + ho + 4),
                  ml = rd32(P, b + ho + 8);
-  const uint32_t m = b + ho + 12;
-  const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4);
+  const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4), ws = rd32(P, m + 13);  // ws: window 0's byte count
   bool ok = (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= d.fs && nwr >= 2 &&
-            nwr <= TABN && ml == 8 + 9 * nwr + 24 && Lb == LBWR;
+            nwr <= TABN && ml == 8 + 9 * nwr + 24 && Lb <= LBWR && Lb >= 34 + 8 && ws >= 256 && ws <= 4096 &&
+            (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwr;
   const uint32_t nwin = ok ? nwr : 2;
-  // lane l: windows 5l..5l+4 = 45 bytes at e0 (m + 8 + 45 * 63 + 48 < 4096);
-  // window q's header: [T min][u8 bits][u32 bytes] at e0 + 9 q.  Two passes
-  // (sizes and checks; then, after the scan, the table entries) so that few
-  // values stay live (the kernel runs at 64 VGPRs).
-  const uint32_t e0 = m + 8 + 45 * l;
-  const uint32_t ws = __builtin_amdgcn_readfirstlane(rd32(P, m + 8 + 5));  // window 0's byte count
-  ok = ok && ws >= 256 && ws <= 4096 && (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwin;
-  auto win = [&](uint32_t q, uint32_t& kind, uint32_t& cs, uint32_t& mn, bool& bad) {
-    const uint32_t wi = 5 * l + q;
-    const uint32_t vmin = rd32(P, e0 + 9 * q), bits = rd32(P, e0 + 9 * q + 4) & 0xffu, nb = rd32(P, e0 + 9 * q + 5);
-    const bool in = wi < nwin;
-    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
-    bad = (in && nb != want);
-    const bool raw = bits >= 32 || (nb & 3) != 0;
-    bad = bad || (in && !raw && bits != 8 && bits != 16);
-    kind = raw ? 2 : bits == 8 ? 0 : 1;
-    cs = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
-    mn = raw ? 0 : vmin;
+  // window q's header: [T min][u8 bits][u32 bytes] at e0 + 9 q
+  const uint32_t sh = e0 & 3;
+  // (the byte shift sh + (o & 3) may reach 6: alignbyte takes it mod 4, so
+  // the dword index steps by hand)
+  auto rw = [&](int o) -> uint32_t {
+    const uint32_t lo0 = R[o >> 2], hi0 = R[(o >> 2) + 1], hi1 = R[(o >> 2) + 2];
+    const uint32_t s = sh + (uint32_t)(o & 3);
+    return s < 4 ? __builtin_amdgcn_alignbyte(hi0, lo0, s) : __builtin_amdgcn_alignbyte(hi1, hi0, s - 4);
   };
-  uint32_t s5 = 0;
+  uint32_t cs[5], kind[5], mn[5];
   bool bad = false;
 #pragma unroll
-  for (uint32_t q = 0; q < 5; q++) {
-    uint32_t kd, c, mv;
-    bool bq;
-    win(q, kd, c, mv, bq);
-    s5 += c;
-    bad = bad || bq;
+  for (int q = 0; q < 5; q++) {
+    const uint32_t wi = 5 * l + q;
+    const uint32_t vmin = rw(9 * q), bits = rw(9 * q + 4) & 0xffu, nb = rw(9 * q + 5);
+    const bool in = wi < nwin;
+    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+    bad = bad || (in && nb != want);
+    const bool raw = bits >= 32 || (nb & 3) != 0;
+    bad = bad || (in && !raw && bits != 8 && bits != 16);
+    kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
+    cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+    mn[q] = raw ? 0 : vmin;
   }
+  const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
   const uint32_t inc = wave_incscan_u32(s5);
   ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
   const uint32_t dst = ho + 12 + ml;  // image offset of the BWR data
   {
     uint32_t off = dst + inc - s5;
 #pragma unroll
-    for (uint32_t q = 0; q < 5; q++) {
-      uint32_t kd, c, mv;
-      bool bq;
-      win(q, kd, c, mv, bq);
-      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kd << 20), mv);
-      off += c;
+    for (int q = 0; q < 5; q++) {
+      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kind[q] << 20), mn[q]);
+      off += cs[q];
     }
   }
-  // compression frame md (compression_filter.cc:413-486): 1 md part of 8 B
-  // (the byteshuffle header) compressed to 17 B, 1 data part of 65,536 B
-  // compressed to 9 + 65,536 B (raw DoubleDelta)
+  // ---- round 2: the compression frame md (compression_filter.cc:413-486):
+  // 1 md part of 8 B (the byteshuffle header) compressed to 17 B, 1 data part
+  // of 65,536 B compressed to d5 bytes (the BWR output is c0 + c1); the DD
+  // headers = BWR-output bytes [0, 34): lane e decodes element e < 9 of
+  // window 0
+  const uint32_t k0 = __builtin_amdgcn_readfirstlane(kind[0]), mn0 = __builtin_amdgcn_readfirstlane(mn[0]);
   const uint32_t f = m + 8 + 9 * nwin;
-  ok = ok && rd32(P, f) == 1 && rd32(P, f + 4) == 1 && rd32(P, f + 8) == 8 && rd32(P, f + 12) == 17 &&
-       rd32(P, f + 16) == OUTB && rd32(P, f + 20) == 9 + OUTB;
-  // DD headers = BWR-output bytes [0, 26): elements 0..6 of window 0 (lane e
-  // decodes element e)
-  uint32_t k0, mn0;
-  {
-    uint32_t c;
-    bool bq;
-    win(0, k0, c, mn0, bq);
-    k0 = __builtin_amdgcn_readfirstlane(k0);
-    mn0 = __builtin_amdgcn_readfirstlane(mn0);
-  }
-  const uint32_t e = l < 7 ? l : 6;
-  uint32_t v;
-  if (k0 == 2) v = rd32(P, b + dst + 4 * e);
-  else if (k0 == 0) v = ext<SGN>(rd32(P, b + dst + e), 0, 8) + mn0;
-  else v = ext<SGN>(rd32(P, b + dst + 2 * e), 0, 16) + mn0;
+  const uint32_t lf = l < 6 ? l : 5;
+  const uint32_t fv = rd32(P, f + 4 * lf);  // lane i < 6: frame dword i
+  const uint32_t e = l < 9 ? l : 8;
+  uint32_t v = rd32(P, b + dst + (e << k0));
+  v = k0 == 2 ? v : (k0 == 0 ? ext<SGN>(v, 0, 8) : ext<SGN>(v, 0, 16)) + mn0;
+  auto fr = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(fv, k); };
+  const uint32_t d5 = fr(5);
+  ok = ok && fr(0) == 1 && fr(1) == 1 && fr(2) == 8 && fr(3) == 17 && fr(4) == OUTB && d5 + 17 == Lb;
   auto dw = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(v, k); };
-  auto at = [&](int o) -> uint32_t { return __builtin_amdgcn_alignbyte(dw((o >> 2) + 1), dw(o >> 2), o & 3); };
+  auto dd = [&](int o) -> uint32_t { return __builtin_amdgcn_alignbyte(dw((o >> 2) + 1), dw(o >> 2), o & 3); };
   // c0 = [u8 bitsize][u64 n = 2][1][65536] (any bitsize: two values, or the
-  // same 8 bytes copied raw); c1 = [u8 bitsize >= 31][u64 16384] + raw values
-  ok = ok && at(1) == 2 && at(5) == 0 && at(9) == 1 && at(13) == OUTB && (at(17) & 0xffu) >= 31 &&
-       at(18) == OUTB / 4 && at(22) == 0;
+  // same 8 bytes copied raw); c1 = [u8 bitsize][u64 16384] followed by the
+  // raw values (bitsize >= 31, dd_compressor.cc:233-236) or by [x0][x1] and
+  // 16,382 codes of bitsize + 1 bits in u64 words, MSB first (bitsize 1..30,
+  // dd_compressor.cc:314-404)
+  const uint32_t bs = dd(17) & 0xffu;
+  const uint32_t cb = bs + 1, words = ((OUTB / 4 - 2) * cb + 63) / 64;
+  const bool raw = bs >= 31;
+  ok = ok && dd(1) == 2 && dd(5) == 0 && dd(9) == 1 && dd(13) == OUTB && dd(18) == OUTB / 4 && dd(22) == 0 &&
+       (raw ? d5 == 9 + OUTB : bs >= 1 && d5 == 17 + 8 * words);
   if (l == 0) {
     L.hd[0] = ok ? 1u : 0u;
     L.hd[1] = 31 - __builtin_clz(ws);
     L.hd[2] = nwin - 1;
+    L.hd[3] = raw ? 0u : cb;
+    L.hd[4] = dd(26);
+    L.hd[5] = dd(30);
   }
 }
 
@@ -344,6 +354,211 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
   }
 }
 
+// ---------------------------------------------------------------------------
+// coded DoubleDelta tiles (bitsize 1..30)
+// ---------------------------------------------------------------------------
+// Thread T owns DD values 16 T .. 16 T + 15 (stream order: plane K = T / 256,
+// so each wave's 1,024 values are one block of the scan), i.e. codes
+// 16 T - 2 .. 16 T + 13 of the stream (values 0 and 1 are the header's x0
+// and x1, which enter as pseudo codes x0 and x1 - 2 x0).  The codes' bits
+// lie in BWR-output elements (dwords) es .. es + 19; the lane decodes those
+// 20 elements straight from the image (two window entries per lane: 20
+// elements span at most two windows of >= 64), realigns them into the
+// MSB-first code stream and extracts its 16 codes at compile-time bit
+// positions (one instantiation per code width CB = bitsize + 1).
+
+// DD^-1 codes of one lane (CB = bitsize + 1).  H: the dwords at byte 2 of
+// the lane's 20 BWR elements (the stream's u64 words start at BWR-output byte
+// 34: word q = bytes [34 + 8 q, 42 + 8 q)); the MSB-first dword sequence
+// swaps the halves of every word.  p: parity of the first dword, n: alignbit
+// amount (dd_compressor.cc:384-399 reads a code as 1 sign bit + bitsize
+// magnitude bits).
+template <int CB>
+__device__ __forceinline__ void dd_codes(const uint32_t (&H)[18], uint32_t p, uint32_t n, bool first,
+                                         uint32_t x0, uint32_t x1, uint32_t (&xl)[16], uint32_t& Aout,
+                                         uint32_t& Bout) {
+  uint32_t pm = 0u - p;
+  asm volatile("" : "+v"(pm));  // (opaque: the select stays one v_bfi_b32)
+  uint32_t M[17];
+#pragma unroll
+  for (int j = 0; j < 17; j++) M[j] = (pm & H[(j + 1) ^ 1]) | (~pm & H[j ^ 1]);
+  uint32_t A[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) A[j] = __builtin_amdgcn_alignbit(M[j], M[j + 1], n);
+  constexpr int B = CB - 1;
+  uint32_t drun = 0, xrun = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int pos = i * CB;
+    const int j = pos >> 5, o = pos & 31;
+    const int32_t sg = __builtin_amdgcn_sbfe((int32_t)A[j], 31 - o, 1);
+    const int o1a = o + 1;
+    const int jm = j + (o1a >> 5), o1 = o1a & 31;
+    uint32_t mag;
+    if (o1 + B <= 32) {
+      mag = __builtin_amdgcn_ubfe(A[jm], 32 - o1 - B, B);
+    } else {
+      mag = __builtin_amdgcn_alignbit(A[jm], A[jm + 1], 64 - o1 - B) & ((1u << B) - 1u);
+    }
+    uint32_t dd = (mag ^ (uint32_t)sg) - (uint32_t)sg;
+    if (i == 0) dd = first ? x0 : dd;
+    if (i == 1) dd = first ? x1 - 2u * x0 : dd;
+    drun += dd;
+    xrun += drun;
+    xl[i] = xrun;
+  }
+  Aout = drun;
+  Bout = xrun;
+}
+
+// DD aggregate combine: the block with aggregate (Ap, Bp) precedes `self`
+// (nself codes): B = Bp + nself * Ap + B, A = Ap + A.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nself) {
+  const uint32_t Ap = dpp0<CTRL, ROWS>(A), Bp = dpp0<CTRL, ROWS>(B);
+  B = B + Bp + nself * Ap;
+  A = A + Ap;
+}
+
+// BWR^-1 of the lane's 20 elements es .. es + 19 (the elements past the
+// last window decode as anything: they only feed bits past the stream)
+template <bool SGN>
+__device__ __forceinline__ void coded_elements(const Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t es,
+                                               uint32_t (&G)[20]) {
+  uint32_t wa = es >> esh, wb = (es + 19) >> esh;
+  wa = wa < wlast ? wa : wlast;
+  wb = wb < wlast ? wb : wlast;
+  const uint2 ta = L.TAB[wa], tb = L.TAB[wb];
+  const uint32_t eb = wb > wa ? wb << esh : 0xffffffffu, ea = wa << esh;
+#pragma unroll
+  for (int x = 0; x < 20; x++) {
+    const uint32_t e = es + x;
+    const bool hi = e >= eb;
+    const uint32_t tx = hi ? tb.x : ta.x, st = hi ? eb : ea, kind = tx >> 20;
+    uint32_t o = (tx & OFFM) + ((e - st) << kind) + b;
+    o = o < IMGU * 16 - 8 ? o : IMGU * 16 - 8;
+    G[x] = rd32(L.IMG, o);
+  }
+#pragma unroll
+  for (int x = 0; x < 20; x++) {
+    const uint32_t e = es + x;
+    const bool hi = e >= eb;
+    const uint32_t tx = hi ? tb.x : ta.x, mn = hi ? tb.y : ta.y, kind = tx >> 20;
+    const uint32_t v = (kind == 0 ? ext<SGN>(G[x], 0, 8) : ext<SGN>(G[x], 0, 16)) + mn;
+    G[x] = kind == 2 ? G[x] : v;
+  }
+}
+
+// The lane's 16 values (local running sums) and its exclusive wave prefix
+// (ae, be); lane 63 publishes the wave total.
+template <int CB, bool SGN>
+__device__ __forceinline__ void coded_lane(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w, uint32_t l,
+                                           uint32_t x0, uint32_t x1, uint32_t (&xk)[16], uint32_t& ae,
+                                           uint32_t& be) {
+  const int32_t T = (int32_t)(64 * w + l);
+  const int32_t P0 = (16 * T - 2) * CB;  // stream bit of the lane's first code
+  const int32_t b0 = (P0 + 31) >> 5;
+  const uint32_t n = (uint32_t)(32 * b0 - P0);
+  const int32_t Ms = b0 - 1;              // first MSB-first stream dword needed
+  const uint32_t p = (uint32_t)Ms & 1u;
+  const uint32_t es = (uint32_t)(8 + 2 * (Ms >> 1));
+  uint32_t G[20];
+  coded_elements<SGN>(L, b, esh, wlast, es, G);
+  uint32_t H[18];
+#pragma unroll
+  for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
+  uint32_t A = 0, B = 0;
+  dd_codes<CB>(H, p, n, T == 0, x0, x1, xk, A, B);
+  const uint32_t As = A, Bs = B;
+  scan_step<DPP_ROW_SHR1, 0xf>(A, B, 16);
+  scan_step<DPP_ROW_SHR2, 0xf>(A, B, 32);
+  scan_step<DPP_ROW_SHR4, 0xf>(A, B, 64);
+  scan_step<DPP_ROW_SHR8, 0xf>(A, B, 128);
+  scan_step<DPP_ROW_BCAST15, 0xa>(A, B, 16 * ((l & 15) + 1));
+  scan_step<DPP_ROW_BCAST31, 0xc>(A, B, 16 * ((l & 31) + 1));
+  ae = A - As;
+  be = B - Bs - 16 * (A - As);
+  if (l == 63) {
+    L.red[w][0] = A;
+    L.red[w][1] = B;
+  }
+}
+
+// LDS dword of DD value v in the value buffer (written by its owner as four
+// 16-B slots, slot q of thread T at 4 T + (q ^ ((T >> 2) & 3)): the b128
+// writes of lanes T and T + 4 do not share banks)
+__device__ __forceinline__ uint32_t vslot(uint32_t v) {
+  const uint32_t T = v >> 4, q = (v >> 2) & 3;
+  return 4 * (4 * T + (q ^ ((T >> 2) & 3))) + (v & 3);
+}
+
+// A coded tile: codes, scans (one barrier publishes the 16 wave totals and
+// frees the image), the fold of each lane's prefix into its values, the
+// values into LDS (second barrier), then byteshuffle^-1 and the stores.
+template <int CB, bool SGN, int ABL>
+__device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, uint32_t esh, uint32_t wlast,
+                                           uint32_t w, uint32_t l, uint64_t* prof) {
+  const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
+  uint32_t xk[16], ae, be;
+  const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  coded_lane<CB, SGN>(L, b, esh, wlast, w, l, x0, x1, xk, ae, be);
+  const uint64_t c4 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  lds_barrier();
+  // the start state (X, D) of this wave's block: the exclusive fold of the
+  // waves before it (1,024 codes each); lane v < 16 holds wave v's total and
+  // a DPP scan over the 16 lanes does the fold
+  uint32_t X, Dd;
+  {
+    uint32_t A = l < 16 ? L.red[l][0] : 0u, B = l < 16 ? L.red[l][1] : 0u;
+    const uint32_t As = A, Bs = B;
+    scan_step<DPP_ROW_SHR1, 0xf>(A, B, 1024);
+    scan_step<DPP_ROW_SHR2, 0xf>(A, B, 2048);
+    scan_step<DPP_ROW_SHR4, 0xf>(A, B, 4096);
+    scan_step<DPP_ROW_SHR8, 0xf>(A, B, 8192);
+    // (inclusive over lanes 0..v; exclusive = minus lane v's own block)
+    X = __builtin_amdgcn_readlane(B - Bs - 1024u * (A - As), w);
+    Dd = __builtin_amdgcn_readlane(A - As, w);
+  }
+  uint32_t t = X + be + 16u * l * Dd;
+  const uint32_t st = Dd + ae;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    t += st;
+    xk[i] += t;
+  }
+  const uint32_t T = 64 * w + l;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++)
+    *(v4u*)(L.IMG + 4 * (4 * T + (q ^ ((T >> 2) & 3)))) = v4u{xk[4 * q], xk[4 * q + 1], xk[4 * q + 2], xk[4 * q + 3]};
+  const uint64_t c5 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  lds_barrier();
+  const uint64_t c6 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  uint8_t* const o = d.out + 16u * T;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++) {
+    const uint32_t j = 1024 * r + T;
+    uint32_t x[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) x[k] = L.IMG[vslot(4096 * k + j)];
+    const v4u v = unshuffle4(x);
+    if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
+      __builtin_nontemporal_store(v, (g_u4*)(o + 16384u * r));
+  }
+  if (prof && l == 0 && (w == 0 || w == 15)) {
+    // coded tiles: 2 codes + wave scan, 3 B3 + fold + value writes, 4 B4,
+    // 5 transposes + stores (wave 0; wave 15 in 6)
+    const uint64_t c7 = __builtin_amdgcn_s_memtime();
+    if (w == 0) {
+      prof[2] = c4 - c3;
+      prof[3] = c5 - c4;
+      prof[4] = c6 - c5;
+      prof[5] = c7 - c6;
+    } else {
+      prof[6] = c7 - c3;
+    }
+  }
+}
+
 // ABL (timing ablations, outputs not meaningful): 1 no parse and no decode
 // (DMA, barriers, constant stores), 2 parse but no decode, 3 no stores,
 // 4 every wave on the one-read path, 5 no 8-bit combine
@@ -365,8 +580,12 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   const uint64_t t = (uint64_t)base + j;
   if (t >= work_items(kp)) return;
   const bool chunked = kp.chunks != nullptr;
+  // the fused kernel's fallback queue starts empty for this launch (the
+  // fused kernel runs next on the same stream and is the only one to append;
+  // chunk mode: the directory pass cleared it and may have appended, so fbq
+  // is not passed here)
+  if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const Desc d = load_desc(kp, t);
-  if (d.fs <= SMALL) return;  // the coded kernel's class
   if (!takes(kp, d)) {
     decline(kp, t);
     return;
@@ -384,7 +603,13 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
   const uint64_t c1 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  if (w == 0 && ABL != 1) parse<SGN>(L, d, l, chunked);
+  if (w == 0 && ABL != 1) {
+    // (the other waves wait at the barrier: the parse wave issues first on
+    // its SIMD, ahead of the other workgroup's waves)
+    __builtin_amdgcn_s_setprio(3);
+    parse<SGN>(L, d, l, chunked);
+    __builtin_amdgcn_s_setprio(0);
+  }
   lds_barrier();
   const uint64_t c2 = prof ? __builtin_amdgcn_s_memtime() : 0;
   if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
@@ -393,6 +618,40 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   }
   const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
   const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
+  const uint32_t cb = __builtin_amdgcn_readfirstlane(L.hd[3]);
+  if (cb != 0) {
+    // coded DoubleDelta: one instantiation per code width
+    const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
+    switch (cb) {
+#define TDBG_CB(c) \
+  case c: coded_tile<c, SGN, ABL>(L, d, b, wsh - 2, wlast, w, l, prof); break;
+      TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
+      TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
+      TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
+      TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
+      TDBG_CB(31)
+#undef TDBG_CB
+      default: break;
+    }
+    if (prof && threadIdx.x == 0) {
+      prof[0] = c1 - c0;
+      prof[1] = c2 - c1;
+    }
+    if (threadIdx.x == 0) {
+      if (kp.status && !chunked) kp.status[t] = TDBG_OK;
+      if (kp.stats) {
+        uint64_t* s = kp.stats + TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63));
+        if (chunked) {
+          atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_CHUNKS], 1ull);
+        } else {
+          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
+          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+          atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
+        }
+      }
+    }
+    return;
+  }
   const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh);
   uint8_t* const o = d.out + 16u * (64 * w + l);
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
@@ -450,7 +709,8 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
 // of at most GRID_CAP items
 extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s) {
   using namespace tdbg::c5t;
-  static const int abl = getenv("TDBG_C5T_ABL") ? atoi(getenv("TDBG_C5T_ABL")) : 0;  // experiments
+#ifdef TDBG_EXPERIMENTS
+  static const int abl = tdbg_hook("TDBG_C5T_ABL") ? atoi(tdbg_hook("TDBG_C5T_ABL")) : 0;  // experiments
   auto k = sgn ? (abl == 1   ? unfilter_c5tile_kernel<true, 1>
                   : abl == 2 ? unfilter_c5tile_kernel<true, 2>
                   : abl == 3 ? unfilter_c5tile_kernel<true, 3>
@@ -459,6 +719,9 @@ extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipSt
                   : abl == 6 ? unfilter_c5tile_kernel<true, 6>
                              : unfilter_c5tile_kernel<true, 0>)
                : unfilter_c5tile_kernel<false, 0>;
+#else
+  auto k = sgn ? unfilter_c5tile_kernel<true, 0> : unfilter_c5tile_kernel<false, 0>;
+#endif
   for (uint64_t base = 0; base < kp->ntiles; base += GRID_CAP) {
     const uint32_t cnt = (uint32_t)std::min<uint64_t>(kp->ntiles - base, GRID_CAP);
     const uint32_t grid = 8 * ((cnt + 7) / 8);

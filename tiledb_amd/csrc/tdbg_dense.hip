@@ -222,6 +222,13 @@ __device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint64_
   }
 }
 
+// a present fragment's validity byte (a fragment given without a validity
+// tile counts as valid)
+__device__ __forceinline__ uint8_t valid_at(const uint8_t* const* validity, uint64_t i, uint64_t pos) {
+  const uint8_t* v = validity ? validity[i] : nullptr;
+  return v ? v[pos] : (uint8_t)1;
+}
+
 __global__ void __launch_bounds__(NT) dense_frag_copy_kernel(const tdbg_dense_frag_config fc, uint64_t ntiles,
                                                              const int64_t* tile_start, const int64_t* frag_dom,
                                                              const uint8_t* const* tiles,
@@ -239,8 +246,29 @@ __global__ void __launch_bounds__(NT) dense_frag_copy_kernel(const tdbg_dense_fr
       const uint8_t* src = f >= 0 ? tiles[t * fc.nfrag + f] + pos * cs : fill;
       copy_bytes(result + rc * cs, src, cs);
       if (fc.nullable && result_validity)
-        result_validity[rc] = f >= 0 ? validity[t * fc.nfrag + f][pos] : (uint8_t)fc.fill_validity;
+        result_validity[rc] = f < 0 ? (uint8_t)fc.fill_validity : valid_at(validity, t * fc.nfrag + f, pos);
     }
+  }
+}
+
+// every result cell starts as the fill value (and the fill validity): cells
+// that no given space tile covers keep it
+__global__ void __launch_bounds__(NT) dense_fill_kernel(uint64_t n, uint64_t cs, const uint8_t* fill, uint8_t* result,
+                                                        uint8_t* result_validity, uint8_t fill_validity) {
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
+    copy_bytes(result + i * cs, fill, cs);
+    if (result_validity) result_validity[i] = fill_validity;
+  }
+}
+
+// var cells: every result cell starts as the fill value's size and bytes
+__global__ void __launch_bounds__(NT) dense_var_fill_kernel(uint64_t n, uint64_t fill_units, const uint8_t* fill,
+                                                            uint64_t* offsets, uint64_t* src,
+                                                            uint8_t* result_validity, uint8_t fill_validity) {
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * NT) {
+    offsets[i] = fill_units;
+    src[i] = (uint64_t)fill;
+    if (result_validity) result_validity[i] = fill_validity;
   }
 }
 
@@ -253,10 +281,12 @@ __global__ void __launch_bounds__(NT) dense_var_sizes_kernel(const tdbg_dense_fr
                                                              const uint8_t* const* var_tiles,
                                                              const uint8_t* const* validity, const uint8_t* fill,
                                                              uint64_t* offsets, uint64_t* src,
-                                                             uint8_t* result_validity) {
+                                                             uint8_t* result_validity, uint32_t* err) {
   const tdbg_dense_copy_config& cfg = fc.base;
   const uint64_t div = fc.elements_mode ? fc.data_type_size : 1;
   const uint64_t fill_units = fc.fill_size / div;
+  uint64_t tcells = 1;  // cells per tile: the offsets tile's last entry is the var tile's size
+  for (uint32_t d = 0; d < cfg.dim_num; d++) tcells *= (uint64_t)cfg.tile_extent[d];
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     Region R;
     if (!region_of(cfg, tile_start + t * cfg.dim_num, R)) continue;
@@ -266,14 +296,22 @@ __global__ void __launch_bounds__(NT) dense_var_sizes_kernel(const tdbg_dense_fr
       if (f >= 0) {
         const uint64_t* o = (const uint64_t*)off_tiles[t * fc.nfrag + f];
         const uint64_t o0 = o[pos], o1 = o[pos + 1];
-        offsets[rc] = (o1 - o0) / div;
-        src[rc] = (uint64_t)(var_tiles[t * fc.nfrag + f] + o0);
+        if (o0 <= o1 && o1 <= o[tcells]) {
+          offsets[rc] = (o1 - o0) / div;
+          src[rc] = (uint64_t)(var_tiles[t * fc.nfrag + f] + o0);
+        } else {
+          // offsets outside the var tile: no read past it; the read fails
+          // (TDBG_E_DATA_READ) when the caller checks err
+          offsets[rc] = 0;
+          src[rc] = (uint64_t)fill;
+          if (err) *err = 1;
+        }
       } else {
         offsets[rc] = fill_units;
         src[rc] = (uint64_t)fill;
       }
       if (fc.nullable && result_validity)
-        result_validity[rc] = f >= 0 ? validity[t * fc.nfrag + f][pos] : (uint8_t)fc.fill_validity;
+        result_validity[rc] = f < 0 ? (uint8_t)fc.fill_validity : valid_at(validity, t * fc.nfrag + f, pos);
     }
   }
 }
@@ -361,10 +399,16 @@ extern "C" hipError_t tdbg_launch_dense_frag_copy(const tdbg_dense_frag_config* 
                                                   const int64_t* tile_start, const int64_t* frag_dom,
                                                   const uint8_t* const* tiles, const uint8_t* const* validity,
                                                   const uint8_t* fill, uint8_t* result, uint8_t* result_validity,
-                                                  uint32_t grid, hipStream_t s) {
-  if (ntiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(tdbg::dense::dense_frag_copy_kernel, dim3(grid), dim3(tdbg::dense::NT), 0, s, *fc, ntiles,
-                     tile_start, frag_dom, tiles, validity, fill, result, result_validity);
+                                                  uint64_t ncells, uint32_t grid, hipStream_t s) {
+  using namespace tdbg::dense;
+  if (ncells) {
+    const uint32_t fg = (uint32_t)((ncells + NT - 1) / NT < 4096 ? (ncells + NT - 1) / NT : 4096);
+    hipLaunchKernelGGL(dense_fill_kernel, dim3(fg), dim3(NT), 0, s, ncells, (uint64_t)fc->base.cell_size, fill,
+                       result, fc->nullable ? result_validity : nullptr, (uint8_t)fc->fill_validity);
+  }
+  if (ntiles)
+    hipLaunchKernelGGL(dense_frag_copy_kernel, dim3(grid), dim3(NT), 0, s, *fc, ntiles, tile_start, frag_dom, tiles,
+                       validity, fill, result, result_validity);
   return hipGetLastError();
 }
 
@@ -375,11 +419,17 @@ extern "C" hipError_t tdbg_launch_dense_var_offsets(const tdbg_dense_frag_config
                                                     const uint8_t* const* validity, const uint8_t* fill,
                                                     uint64_t* offsets, uint64_t ncells, uint64_t* src,
                                                     uint8_t* result_validity, uint64_t* bsum, uint64_t* total,
-                                                    uint32_t grid, hipStream_t s) {
+                                                    uint32_t* err, uint32_t grid, hipStream_t s) {
   using namespace tdbg::dense;
+  if (ncells) {
+    const uint32_t fg = (uint32_t)((ncells + NT - 1) / NT < 4096 ? (ncells + NT - 1) / NT : 4096);
+    const uint64_t div = fc->elements_mode ? fc->data_type_size : 1;
+    hipLaunchKernelGGL(dense_var_fill_kernel, dim3(fg), dim3(NT), 0, s, ncells, (uint64_t)fc->fill_size / div, fill,
+                       offsets, src, fc->nullable ? result_validity : nullptr, (uint8_t)fc->fill_validity);
+  }
   if (ntiles)
     hipLaunchKernelGGL(dense_var_sizes_kernel, dim3(grid), dim3(NT), 0, s, *fc, ntiles, tile_start, frag_dom,
-                       off_tiles, var_tiles, validity, fill, offsets, src, result_validity);
+                       off_tiles, var_tiles, validity, fill, offsets, src, result_validity, err);
   const uint64_t nb = (ncells + SB - 1) / SB;
   if (nb) hipLaunchKernelGGL(scan_sums_kernel, dim3((uint32_t)nb), dim3(NT), 0, s, offsets, ncells, bsum);
   hipLaunchKernelGGL(scan_prefix_kernel, dim3(1), dim3(NT), 0, s, bsum, nb, total);

@@ -23,6 +23,7 @@
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
 #include "tdbg_launch.h"
+#include "tdbg_hooks.h"
 
 namespace tdbg {
 thread_local EvArm ev_arm{nullptr, nullptr};  // tdbg_launch.h
@@ -73,14 +74,14 @@ extern "C" hipError_t tdbg_launch_dense_frag_copy(const tdbg_dense_frag_config* 
                                                   const int64_t* tile_start, const int64_t* frag_dom,
                                                   const uint8_t* const* tiles, const uint8_t* const* validity,
                                                   const uint8_t* fill, uint8_t* result, uint8_t* result_validity,
-                                                  uint32_t grid, hipStream_t s);
+                                                  uint64_t ncells, uint32_t grid, hipStream_t s);
 extern "C" hipError_t tdbg_launch_dense_var_offsets(const tdbg_dense_frag_config* fc, uint64_t ntiles,
                                                     const int64_t* tile_start, const int64_t* frag_dom,
                                                     const uint8_t* const* off_tiles, const uint8_t* const* var_tiles,
                                                     const uint8_t* const* validity, const uint8_t* fill,
                                                     uint64_t* offsets, uint64_t ncells, uint64_t* src,
                                                     uint8_t* result_validity, uint64_t* bsum, uint64_t* total,
-                                                    uint32_t grid, hipStream_t s);
+                                                    uint32_t* err, uint32_t grid, hipStream_t s);
 extern "C" hipError_t tdbg_launch_dense_var_copy(const uint64_t* offsets, const uint64_t* src, uint64_t ncells,
                                                  const uint64_t* total, uint64_t mult, uint8_t* var_out,
                                                  uint32_t grid, hipStream_t s);
@@ -189,6 +190,7 @@ struct tdbg_context {
   uint64_t* dense_src = nullptr;
   uint64_t dense_src_cap = 0, dense_ncells = 0;
   uint64_t* dense_bsum = nullptr;
+  uint32_t* dense_err = nullptr;  // set by the var sizes kernel: offsets outside their var tile
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -596,6 +598,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->dir_need) (void)hipHostFree((void*)c->dir_need);
   if (c->dense_src) (void)hipFree(c->dense_src);
   if (c->dense_bsum) (void)hipFree(c->dense_bsum);
+  if (c->dense_err) (void)hipFree(c->dense_err);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -634,7 +637,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   kp.flags = flags;
   kp.plan = p->plan;
   {
-    static const char* dbg = getenv("TDBG_DEBUG_STOP");  // timing-only ablation
+    static const char* dbg = tdbg_hook("TDBG_DEBUG_STOP");  // timing-only ablation
     kp.dbg_stop = dbg ? (uint32_t)atoi(dbg) : 0;
   }
   const bool fast = !force_general && p->plan.fast != 0;
@@ -655,7 +658,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   kp.md_cap = c->md_cap;
   kp.tab_cap = c->tab_cap;
   {
-    static const bool prof = getenv("TDBG_PROF") != nullptr;
+    static const bool prof = tdbg_hook("TDBG_PROF") != nullptr;
     if (prof && fast) {
       const uint32_t pgrid = std::max<uint32_t>(grid, tdbg_stream_grid(c->cus));
       if (c->prof_grid < pgrid) {
@@ -679,7 +682,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // Chunk-parallel: asked for, or fewer tiles than CUs (tiles, not chunks,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
-  static const bool tile_mode = getenv("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
+  static const bool tile_mode = tdbg_hook("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
   const bool chunked = queued && !d_list &&
                        ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
   // [BYTESHUFFLE] on 4-byte values (C1): the unit-parallel streaming kernel
@@ -690,8 +693,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // The headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BWR] on 4-byte
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
-  static const bool no_stream = getenv("TDBG_NO_STREAM") != nullptr;  // ablation
-  static const bool c5_old_raw = getenv("TDBG_C5_OLD_RAW") != nullptr;  // A/B: the persistent raw-DD kernel
+  static const bool no_stream = tdbg_hook("TDBG_NO_STREAM") != nullptr;  // ablation
+  static const bool c5_old_raw = tdbg_hook("TDBG_C5_OLD_RAW") != nullptr;  // A/B: the persistent raw-DD kernel
   const bool c5_stream = (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
                          p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
   // The scan pipelines of C3a / C3b / C4 on 8-byte values first go through
@@ -788,8 +791,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   };
   if (te) tdbg::ev_arm.start = te[0];
   hipError_t e = hipSuccess;
-  static const bool skip_fused = getenv("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
-  static const bool skip_fixup = getenv("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
+  static const bool skip_fused = tdbg_hook("TDBG_DEBUG_SKIP_FUSED") != nullptr;  // ablation
+  static const bool skip_fixup = tdbg_hook("TDBG_DEBUG_SKIP_FIXUP") != nullptr;  // ablation
   if (chunk_stream) {
     const uint32_t cap = (uint32_t)std::min<uint64_t>(c->cq_cap, 0xffffffffull);
     tdbg::KParams ks = kp;
@@ -805,10 +808,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
     } else {
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
-      if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
-      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
-      if (!skip_fused) e = c5_old_raw ? tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream)
-                                      : tdbg_launch_c5tile(&ks, sgn, stream);
+      if (c5_old_raw) {
+        if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
+        if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+        if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      } else if (!skip_fused) {
+        e = tdbg_launch_c5tile(&ks, sgn, stream);
+      }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
     tdbg::KParams kf = kp;  // the fused kernel on the chunks they queued
@@ -833,10 +839,13 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
     } else {
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
-      if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
-      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
-      if (!skip_fused) e = c5_old_raw ? tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream)
-                                      : tdbg_launch_c5tile(&ks, sgn, stream);
+      if (c5_old_raw) {
+        if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
+        if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
+        if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
+      } else if (!skip_fused) {
+        e = tdbg_launch_c5tile(&ks, sgn, stream);
+      }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
     tdbg::KParams kf = kp;  // the fused kernel on the streaming kernel's queue
@@ -1090,7 +1099,7 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
   // LDS-resident forward kernel (tdbg_forward_stream.hip); the tiles it does
   // not take (other sizes, alignments, capacities) are queued in the fused
   // fallback queue for the general forward kernel, which runs on the queue.
-  static const bool no_fast = getenv("TDBG_NO_FWD_STREAM") != nullptr;  // ablation
+  static const bool no_fast = tdbg_hook("TDBG_NO_FWD_STREAM") != nullptr;  // ablation
   const tdbg_plan& P = p->plan;
   const bool c5 = !no_fast && !d_list && (P.fast == 19 || P.fast == 20) && P.nstages == 3 && P.s[0].w == 4 &&
                   P.s[1].w == 4 && P.s[2].w == 4 && P.s[2].dts == 4 && P.s[1].sgn == P.s[2].sgn &&
@@ -1157,7 +1166,7 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kf.fbq = c->d_fbq;
     kf.fbq_cap = (uint32_t)n;
     kf.stats = c->d_stats;
-    static const bool prof = getenv("TDBG_PROF") != nullptr;  // diagnostics: phase clocks
+    static const bool prof = tdbg_hook("TDBG_PROF") != nullptr;  // diagnostics: phase clocks
     const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
     if (prof) {
       if (c->prof_grid < fgrid) {
@@ -1808,6 +1817,32 @@ int tdbg_dense_copy_async(tdbg_context* c, const tdbg_dense_copy_config* cfg, ui
   return TDBG_OK;
 }
 
+// Host-side check of a dense read's space tiles (tile_start on the host): on
+// one grid (tile 0's start as origin), distinct, and their intersections with
+// the subarray add up to the whole subarray -- every result cell comes from
+// exactly one given tile.  Returns nullptr when they do, else the reason.
+static const char* dense_tiles_cover(const tdbg_dense_copy_config* cfg, uint64_t ntiles, const int64_t* tile_start) {
+  const uint32_t nd = cfg->dim_num;
+  uint64_t want = 1, got = 0;
+  for (uint32_t d = 0; d < nd; d++) want *= (uint64_t)(cfg->sub_hi[d] - cfg->sub_lo[d] + 1);
+  std::vector<std::vector<int64_t>> keys(ntiles);
+  for (uint64_t t = 0; t < ntiles; t++) {
+    uint64_t n = 1;
+    for (uint32_t d = 0; d < nd; d++) {
+      const int64_t s = tile_start[t * nd + d], e = cfg->tile_extent[d];
+      if ((s - tile_start[d]) % e != 0) return "dense read: tile start off the tile grid";
+      const int64_t lo = std::max(s, cfg->sub_lo[d]), hi = std::min(s + e - 1, cfg->sub_hi[d]);
+      n = hi < lo ? 0 : n * (uint64_t)(hi - lo + 1);
+    }
+    got += n;
+    keys[t].assign(tile_start + t * nd, tile_start + (t + 1) * nd);
+  }
+  std::sort(keys.begin(), keys.end());
+  if (std::adjacent_find(keys.begin(), keys.end()) != keys.end()) return "dense read: a tile is given twice";
+  if (got != want) return "dense read: the tiles do not cover the subarray";
+  return nullptr;
+}
+
 int tdbg_dense_read_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles, const uint8_t* const* in,
                          const uint64_t* in_size, const int64_t* tile_start, const tdbg_dense_copy_config* cfg,
                          uint8_t* result, uint64_t result_size, uint32_t flags, int32_t* host_status,
@@ -1819,31 +1854,9 @@ int tdbg_dense_read_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntile
   if (!result || result_size < rbytes) return fail(TDBG_E_ARG, "result buffer smaller than the subarray");
   if (ntiles == 0) return TDBG_OK;
   if (!in || !in_size || !tile_start) return fail(TDBG_E_ARG, "null tile arrays");
-  {
-    // Every result cell must come from a tile (this entry has no fill value,
-    // and the device result buffer is not initialised): the tiles lie on one
-    // grid (tile 0's start as origin), are distinct, and their intersections
-    // with the subarray add up to the whole subarray.
-    const uint32_t nd = cfg->dim_num;
-    uint64_t want = 1, got = 0;
-    for (uint32_t d = 0; d < nd; d++) want *= (uint64_t)(cfg->sub_hi[d] - cfg->sub_lo[d] + 1);
-    std::vector<std::vector<int64_t>> keys(ntiles);
-    for (uint64_t t = 0; t < ntiles; t++) {
-      uint64_t n = 1;
-      for (uint32_t d = 0; d < nd; d++) {
-        const int64_t s = tile_start[t * nd + d], e = cfg->tile_extent[d];
-        if ((s - tile_start[d]) % e != 0) return fail(TDBG_E_ARG, "dense read: tile start off the tile grid");
-        const int64_t lo = std::max(s, cfg->sub_lo[d]), hi = std::min(s + e - 1, cfg->sub_hi[d]);
-        n = hi < lo ? 0 : n * (uint64_t)(hi - lo + 1);
-      }
-      got += n;
-      keys[t].assign(tile_start + t * nd, tile_start + (t + 1) * nd);
-    }
-    std::sort(keys.begin(), keys.end());
-    if (std::adjacent_find(keys.begin(), keys.end()) != keys.end())
-      return fail(TDBG_E_ARG, "dense read: a tile is given twice");
-    if (got != want) return fail(TDBG_E_ARG, "dense read: the tiles do not cover the subarray");
-  }
+  // Every result cell must come from a tile (this entry has no fill value,
+  // and the device result buffer is not initialised)
+  if (const char* why = dense_tiles_cover(cfg, ntiles, tile_start)) return fail(TDBG_E_ARG, why);
   HIP_OK(hipSetDevice(c->device));
   if (batch_bytes == 0) batch_bytes = 256ull << 20;
   const bool cin = (flags & TDBG_HOST_CONTIGUOUS_INPUT) != 0;
@@ -2051,17 +2064,16 @@ int tdbg_dense_copy_fragments_async(tdbg_context* c, const tdbg_dense_frag_confi
                                     tdbg_stream stream) {
   if (!c) return fail(TDBG_E_ARG, "null context");
   if (!frag_cfg_ok(cfg, false)) return fail(TDBG_E_ARG, "invalid dense fragment copy config");
-  if (ntiles == 0) return TDBG_OK;
-  if (!d_tile_start || !d_result || !d_fill_value || (cfg->nfrag && (!d_tiles || !d_frag_dom)))
+  if (!d_result || !d_fill_value || (ntiles && !d_tile_start) || (ntiles && cfg->nfrag && (!d_tiles || !d_frag_dom)))
     return fail(TDBG_E_ARG, "null dense copy arrays");
-  if (cfg->nullable && (!d_result_validity || (cfg->nfrag && !d_validity)))
-    return fail(TDBG_E_ARG, "nullable copy without validity buffers");
+  if (cfg->nullable && !d_result_validity) return fail(TDBG_E_ARG, "nullable copy without a result validity buffer");
   HIP_OK(hipSetDevice(c->device));
   int rc = order_stream(c, (hipStream_t)stream);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
   hipError_t e = tdbg_launch_dense_frag_copy(cfg, ntiles, d_tile_start, d_frag_dom, d_tiles, d_validity, d_fill_value,
-                                             d_result, d_result_validity, grid, (hipStream_t)stream);
+                                             d_result, d_result_validity, dense_cells(&cfg->base), std::max(grid, 1u),
+                                             (hipStream_t)stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense copy launch: ") + hipGetErrorString(e));
   return TDBG_OK;
 }
@@ -2077,11 +2089,14 @@ int tdbg_dense_var_offsets_async(tdbg_context* c, const tdbg_dense_frag_config* 
   if (!d_result_offsets || !d_var_total || !d_fill_value || (ntiles && !d_tile_start) ||
       (ntiles && cfg->nfrag && (!d_offset_tiles || !d_var_tiles || !d_frag_dom)))
     return fail(TDBG_E_ARG, "null dense var arrays");
-  if (cfg->nullable && (!d_result_validity || (cfg->nfrag && !d_validity)))
-    return fail(TDBG_E_ARG, "nullable copy without validity buffers");
+  if (cfg->nullable && !d_result_validity) return fail(TDBG_E_ARG, "nullable copy without a result validity buffer");
   HIP_OK(hipSetDevice(c->device));
   int rc = order_stream(c, (hipStream_t)stream);
   if (rc) return rc;
+  if (!c->dense_err) {
+    HIP_OK(hipMalloc(&c->dense_err, 4));
+    HIP_OK(hipMemsetAsync(c->dense_err, 0, 4, (hipStream_t)stream));
+  }
   const uint64_t n = dense_cells(&cfg->base);
   const uint64_t nb = (n + 2047) / 2048;
   if (n > c->dense_src_cap) {
@@ -2099,7 +2114,7 @@ int tdbg_dense_var_offsets_async(tdbg_context* c, const tdbg_dense_frag_config* 
   const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), (uint64_t)c->cus * 8);
   hipError_t e = tdbg_launch_dense_var_offsets(cfg, ntiles, d_tile_start, d_frag_dom, d_offset_tiles, d_var_tiles,
                                                d_validity, d_fill_value, d_result_offsets, n, c->dense_src,
-                                               d_result_validity, c->dense_bsum, d_var_total, grid,
+                                               d_result_validity, c->dense_bsum, d_var_total, c->dense_err, grid,
                                                (hipStream_t)stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense var offsets launch: ") + hipGetErrorString(e));
   return TDBG_OK;
@@ -2141,6 +2156,11 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
   if (npair && (!tile_start || !frag_dom || !off_filtered || !off_filtered_size || !var_filtered ||
                 !var_filtered_size || !var_unfiltered_size))
     return fail(TDBG_E_ARG, "null dense var read inputs");
+  if (ntiles && !tile_start) return fail(TDBG_E_ARG, "null dense var read inputs");
+  // every result cell comes from exactly one given space tile (its value or
+  // the fill value), as the reference iterates every space tile of the
+  // subarray
+  if (const char* why = dense_tiles_cover(&cfg->base, ntiles, tile_start)) return fail(TDBG_E_ARG, why);
   HIP_OK(hipSetDevice(c->device));
   if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
   hipStream_t s = c->cstream;
@@ -2238,6 +2258,27 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
     HIP_OK(hipMemcpyAsync(st.data(), d_st, 2 * m * 4, hipMemcpyDeviceToHost, s));
   }
   HIP_OK(hipStreamSynchronize(s));
+  // Tiles a stage outgrew the default scratch slots for (TDBG_E_SCRATCH: tiny
+  // PD/BWR windows, RLE of 1-byte cells, ...): redone one by one through the
+  // sync entry's bigger retry slots, in place (their table rows are one-tile
+  // arrays); an offsets tile then takes its extra offset
+  for (uint64_t k = 0; k < 2 * m; k++) {
+    if (st[k] != TDBG_E_SCRATCH) continue;
+    const bool offs = k < m;
+    int32_t one = 0;
+    rc = tdbg_unfilter_tiles_sync(c, offs ? po : pv, 1, (const uint8_t* const*)(dp + k), dp + 2 * m + k,
+                                  (uint8_t* const*)(dp + 4 * m + k), dp + 6 * m + k, offs ? TDBG_TILE_OFFSETS : 0u,
+                                  &one, (tdbg_stream)s);
+    if (rc != TDBG_OK && one == TDBG_OK) return rc;  // (a launch failure, not a tile status)
+    st[k] = one;
+    if (offs && one == TDBG_OK) {
+      HIP_OK(hipMemsetAsync(d_st + k, 0, 4, s));
+      hipError_t e = tdbg_launch_extra_offset(1, (uint8_t* const*)(dp + 4 * m + k), dp + 6 * m + k, dp + 8 * m + k,
+                                              d_st + k, s);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("extra offset launch: ") + hipGetErrorString(e));
+    }
+  }
+  HIP_OK(hipStreamSynchronize(s));
   // per pair: the first failure of its two tiles; any failure stops the read
   // (an unfilter error fails the reference's query)
   std::vector<int32_t> pst(npair, 0);
@@ -2257,7 +2298,13 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(var_total, d_total, 8, hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(result_offsets, d_roff, n * 8, hipMemcpyDeviceToHost, s));
+  uint32_t herr = 0;
+  HIP_OK(hipMemcpyAsync(&herr, c->dense_err, 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  if (herr) {
+    HIP_OK(hipMemset(c->dense_err, 0, 4));
+    return fail(TDBG_E_DATA_READ, "dense var read: a cell's offsets lie outside its var tile");
+  }
   const uint64_t mult = cfg->elements_mode ? cfg->data_type_size : 1;
   const uint64_t vbytes = *var_total * mult;
   if (vbytes > var_cap || (vbytes && !result_var))

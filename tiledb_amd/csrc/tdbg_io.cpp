@@ -36,6 +36,7 @@
 
 #include "../../include/tiledb_amd.h"
 #include "tdbg_desc.h"
+#include "tdbg_hooks.h"
 
 namespace {
 
@@ -225,7 +226,7 @@ int tdbg_read_unfilter_tiles(tdbg_context* c, const tdbg_pipeline* p, uint64_t n
   std::string err;
   // test hook: block k's unfilter "fails" with a device error before any of
   // its statuses exist (the failure class of a HIP error in the host path)
-  const long fail_block = getenv("TDBG_DEBUG_IO_FAIL_BLOCK") ? atol(getenv("TDBG_DEBUG_IO_FAIL_BLOCK")) : -1;
+  const long fail_block = tdbg_hook("TDBG_DEBUG_IO_FAIL_BLOCK") ? atol(tdbg_hook("TDBG_DEBUG_IO_FAIL_BLOCK")) : -1;
   // every tile is "not processed" until its block's unfilter reports it: a
   // block whose unfilter stops early (a device error before its statuses
   // are copied back), and every block after a device error, keep that

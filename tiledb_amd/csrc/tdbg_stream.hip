@@ -54,6 +54,7 @@
 #include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
+#include "tdbg_hooks.h"
 
 namespace tdbg {
 namespace stream {
@@ -825,7 +826,7 @@ __global__ void __launch_bounds__(NT, TDBG_STREAM_OCC) unfilter_stream_kernel(co
 // Persistent grid: one workgroup per CU for every TDBG_STREAM_OCC waves per
 // SIMD the registers allow (LDS would hold four).
 extern "C" uint32_t tdbg_stream_grid(int cus) {
-  static const int g = getenv("TDBG_STREAM_GRID") ? atoi(getenv("TDBG_STREAM_GRID")) : 0;  // experiments
+  static const int g = tdbg_hook("TDBG_STREAM_GRID") ? atoi(tdbg_hook("TDBG_STREAM_GRID")) : 0;  // experiments
   return g > 0 ? (uint32_t)g : (uint32_t)cus * TDBG_STREAM_OCC;
 }
 
@@ -834,10 +835,10 @@ extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid,
   using namespace tdbg::stream;
   // store mode: 1 nontemporal (5 % faster than plain stores on C5 active,
   // profiles/r03_*), 3 no stores (timing ablation only, signed tiles)
-  static const int stm = getenv("TDBG_STREAM_STORE") ? atoi(getenv("TDBG_STREAM_STORE")) : 1;
+  static const int stm = tdbg_hook("TDBG_STREAM_STORE") ? atoi(tdbg_hook("TDBG_STREAM_STORE")) : 1;
   // one barrier per tile for short launches, one per plane for long ones
   // (planes4); TDBG_STREAM_PB=1|4 forces one (experiments)
-  static const int pbe = getenv("TDBG_STREAM_PB") ? atoi(getenv("TDBG_STREAM_PB")) : 0;
+  static const int pbe = tdbg_hook("TDBG_STREAM_PB") ? atoi(tdbg_hook("TDBG_STREAM_PB")) : 0;
   const bool pb1 = pbe ? pbe == 1 : kp->ntiles < 48ull * grid;
   auto k = stm == 3 ? unfilter_stream_kernel<true, 3, 4>
            : sgn    ? (pb1 ? unfilter_stream_kernel<true, 1, 1> : unfilter_stream_kernel<true, 1, 4>)

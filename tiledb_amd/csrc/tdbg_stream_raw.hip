@@ -45,6 +45,7 @@
 #include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
+#include "tdbg_hooks.h"
 
 namespace tdbg {
 namespace sraw {
@@ -638,13 +639,13 @@ __global__ void __launch_bounds__(NT, TDBG_RAW_OCC) unfilter_stream_raw_kernel(c
 }  // namespace tdbg
 
 extern "C" uint32_t tdbg_stream_raw_grid(int cus) {
-  static const int g = getenv("TDBG_RAW_GRID") ? atoi(getenv("TDBG_RAW_GRID")) : 0;  // experiments
+  static const int g = tdbg_hook("TDBG_RAW_GRID") ? atoi(tdbg_hook("TDBG_RAW_GRID")) : 0;  // experiments
   return g > 0 ? (uint32_t)g : (uint32_t)cus * TDBG_RAW_OCC;
 }
 
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
   using namespace tdbg::sraw;
-  static const int abl = getenv("TDBG_RAW_ABL") ? atoi(getenv("TDBG_RAW_ABL")) : 0;
+  static const int abl = tdbg_hook("TDBG_RAW_ABL") ? atoi(tdbg_hook("TDBG_RAW_ABL")) : 0;
   auto k = sgn ? (abl == 1   ? unfilter_stream_raw_kernel<true, 1>
                   : abl == 2 ? unfilter_stream_raw_kernel<true, 2>
                   : abl == 3 ? unfilter_stream_raw_kernel<true, 3>

@@ -53,6 +53,7 @@
 #include "tdbg_launch.h"
 #include "tdbg_device.h"
 #include "tdbg_stream_common.h"
+#include "tdbg_hooks.h"
 
 namespace tdbg {
 namespace ssm {
@@ -674,7 +675,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
 // BWR stage's integer type is signed
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode) {
   using namespace tdbg::ssm;
-  static const int g = getenv("TDBG_SMALL_GRID") ? atoi(getenv("TDBG_SMALL_GRID")) : 0;  // experiments
+  static const int g = tdbg_hook("TDBG_SMALL_GRID") ? atoi(tdbg_hook("TDBG_SMALL_GRID")) : 0;  // experiments
   const int occ = mode == M_DD ? Occ<M_DD>::v : mode == M_RLE ? Occ<M_RLE>::v : Occ<M_PDBWR>::v;
   return g > 0 ? (uint32_t)g : (uint32_t)(cus * occ);
 }

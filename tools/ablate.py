@@ -4,7 +4,7 @@ import os, subprocess, sys, json
 res = {}
 for stop in ["1", "2", "3", "0"]:
     for var in ["rand", "ramp"]:
-        env = dict(os.environ, TDBG_DEBUG_STOP=stop)
+        env = dict(os.environ, TDBG_DEBUG_STOP=stop, TDBG_LIB="libtiledb_amd_exp.so")  # (hooks: experiments library)
         out = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2", "--variants", var,
                               "--no-cpu-baseline"], env=env, capture_output=True, text=True)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]

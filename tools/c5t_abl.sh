@@ -3,6 +3,8 @@
 # against the persistent raw kernel, one box, alternating; plus the ceiling
 # probe's tile shapes for calibration.  usage: r05_abl.sh <tag>
 set -o pipefail
+# the TDBG_* switches below exist only in the experiments library (tdbg_hooks.h)
+export TDBG_LIB=${TDBG_LIB:-libtiledb_amd_exp.so}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05/abl_${1:-x}
 mkdir -p $OUT

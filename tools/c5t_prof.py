@@ -3,6 +3,7 @@ the bench's 100,000-tile workload.  Run on the GPU box:
   TDBG_PROF=1 python tools/c5t_prof.py rand ramp"""
 import os, sys
 os.environ.setdefault("TDBG_PROF", "1")
+os.environ.setdefault("TDBG_LIB", "libtiledb_amd_exp.so")  # (hooks: experiments library)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np
@@ -11,7 +12,9 @@ import bench
 import workloads as W
 from tiledb_amd import engine
 
-NAMES = ["dma-wait", "parse", "setup", "w0-decode+st", "w1-decode+st", "w15-decode+st", "wg-total"]
+NAMES = (["dma-wait", "parse", "setup", "w0-decode+st", "w1-decode+st", "w15-decode+st", "wg-total"]
+         if "active" not in sys.argv else
+         ["dma-wait", "parse", "codes+scan", "B3+fold+vwrite", "B4", "transp+stores", "w15 codes..end"])
 _ser, _dt, _cs, _, _ = W.config("c5")
 dp = engine.DevicePipeline(_ser, 23, int(_dt), _cs)
 ctx = engine.Context(0)

@@ -2,6 +2,7 @@
 Run on the GPU box:  TDBG_PROF=1 python tools/phase_prof.py"""
 import os, sys
 os.environ.setdefault("TDBG_PROF", "1")
+os.environ.setdefault("TDBG_LIB", "libtiledb_amd_exp.so")  # (hooks: experiments library)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np

@@ -5,6 +5,7 @@ import os
 import sys
 
 os.environ.setdefault("TDBG_PROF", "1")
+os.environ.setdefault("TDBG_LIB", "libtiledb_amd_exp.so")  # (hooks: experiments library)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np

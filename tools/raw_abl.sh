@@ -3,6 +3,8 @@
 # alternating: 0 = product, 4 = walk + prefix + parse + barriers only (no jobs),
 # 3 = no stores.  Outputs are not meaningful under an ablation (no verify).
 set -o pipefail
+# the TDBG_* switches below exist only in the experiments library (tdbg_hooks.h)
+export TDBG_LIB=${TDBG_LIB:-libtiledb_amd_exp.so}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/raw_abl_${1:-x}
 mkdir -p $OUT

@@ -2,6 +2,8 @@
 # Streaming-kernel profile: kernel-trace stats of C5 active with plain and
 # nontemporal stores, then the SQ counter passes (tools/sq_prof.sh layout).
 set -o pipefail
+# the TDBG_* switches below exist only in the experiments library (tdbg_hooks.h)
+export TDBG_LIB=${TDBG_LIB:-libtiledb_amd_exp.so}
 TAG=${1:-x}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/sprof_$TAG
