@@ -68,6 +68,7 @@ constexpr uint32_t TABN = 320;        // BWR windows per chunk (nwin <= 257 for 
 constexpr uint32_t LBWR = 65562;      // BWR output bytes of a raw-DD C5 chunk: 17 + 9 + 65536
 constexpr uint32_t OFFM = (1u << 20) - 1;
 constexpr uint32_t GRID_CAP = 1u << 22;
+constexpr uint32_t PFX = 192;         // 16-B units of the image prefix the parse reads (3 KiB)
 
 struct Lds {
   uint32_t IMG[IMGU * 4];
@@ -219,6 +220,7 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
     L.hd[3] = raw ? 0u : cb;
     L.hd[4] = dd(26);
     L.hd[5] = dd(30);
+    L.hd[6] = Lb;
   }
 }
 
@@ -420,41 +422,61 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
   A = A + Ap;
 }
 
-// BWR^-1 of the lane's 20 elements es .. es + 19 (the elements past the
-// last window decode as anything: they only feed bits past the stream)
+// BWR^-1 of the whole chunk (bit_width_reduction_filter.cc:353-404) into LDS,
+// in place over the image, in 16-B units of 4 elements: thread T decodes
+// units T + 1024 j (j < 4: the coded BWR output is at most 63,514 B = 3,970
+// units).  A unit's 4 elements lie in one window (windows are >= 64
+// elements), looked up per lane.  Per round one wave-uniform decoder: every
+// lane's window 8-bit (most rounds of an active tile: one dword read gives
+// the unit), or the general form (five dwords realigned, then per element
+// the window's kind: raw dword, 8-bit byte or 16-bit half, plus the
+// minimum).  Every compressed read lands in registers before the one
+// barrier after which the decoded units overwrite the image.
 template <bool SGN>
-__device__ __forceinline__ void coded_elements(const Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t es,
-                                               uint32_t (&G)[20]) {
-  uint32_t wa = es >> esh, wb = (es + 19) >> esh;
-  wa = wa < wlast ? wa : wlast;
-  wb = wb < wlast ? wb : wlast;
-  const uint2 ta = L.TAB[wa], tb = L.TAB[wb];
-  const uint32_t eb = wb > wa ? wb << esh : 0xffffffffu, ea = wa << esh;
+__device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w,
+                                                uint32_t l) {
+  v4u dv[4];
+  uint2 te[4];
+  uint32_t ea[4];
 #pragma unroll
-  for (int x = 0; x < 20; x++) {
-    const uint32_t e = es + x;
-    const bool hi = e >= eb;
-    const uint32_t tx = hi ? tb.x : ta.x, st = hi ? eb : ea, kind = tx >> 20;
-    uint32_t o = (tx & OFFM) + ((e - st) << kind) + b;
-    o = o < IMGU * 16 - 8 ? o : IMGU * 16 - 8;
-    G[x] = rd32(L.IMG, o);
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t e = 4 * (1024 * j + 64 * w + l);
+    uint32_t W = e >> esh;
+    W = W < wlast ? W : wlast;
+    te[j] = L.TAB[W];
+    const uint32_t kind = te[j].x >> 20;
+    ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);  // LDS byte of element e's compressed value
   }
 #pragma unroll
-  for (int x = 0; x < 20; x++) {
-    const uint32_t e = es + x;
-    const bool hi = e >= eb;
-    const uint32_t tx = hi ? tb.x : ta.x, mn = hi ? tb.y : ta.y, kind = tx >> 20;
-    const uint32_t v = (kind == 0 ? ext<SGN>(G[x], 0, 8) : ext<SGN>(G[x], 0, 16)) + mn;
-    G[x] = kind == 2 ? G[x] : v;
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t kind = te[j].x >> 20, mn = te[j].y;
+    if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
+      const uint32_t y = rd32(L.IMG, ea[j]);
+      dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
+    } else {
+      const uint32_t* p = L.IMG + (ea[j] >> 2);
+      const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], sh = ea[j] & 3;
+      const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh), r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh), r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+      const bool b8 = kind == 0, raw = kind == 2;
+      // element i: 8-bit -> byte i of r0; 16-bit -> half (i & 1) of r(i >> 1)
+      const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
+      const uint32_t e1 = ext<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
+      const uint32_t e2 = ext<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
+      const uint32_t e3 = ext<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
+      dv[j] = v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
+    }
   }
+  lds_barrier();  // every compressed byte is in registers: the stream may overwrite the image
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
 }
 
 // The lane's 16 values (local running sums) and its exclusive wave prefix
 // (ae, be); lane 63 publishes the wave total.
-template <int CB, bool SGN>
-__device__ __forceinline__ void coded_lane(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w, uint32_t l,
-                                           uint32_t x0, uint32_t x1, uint32_t (&xk)[16], uint32_t& ae,
-                                           uint32_t& be) {
+template <int CB>
+__device__ __forceinline__ void coded_lane(Lds& L, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
+                                           uint32_t (&xk)[16], uint32_t& ae, uint32_t& be) {
   const int32_t T = (int32_t)(64 * w + l);
   const int32_t P0 = (16 * T - 2) * CB;  // stream bit of the lane's first code
   const int32_t b0 = (P0 + 31) >> 5;
@@ -462,8 +484,14 @@ __device__ __forceinline__ void coded_lane(Lds& L, uint32_t b, uint32_t esh, uin
   const int32_t Ms = b0 - 1;              // first MSB-first stream dword needed
   const uint32_t p = (uint32_t)Ms & 1u;
   const uint32_t es = (uint32_t)(8 + 2 * (Ms >> 1));
+  // the lane's 20 elements of the decoded stream (es is even: 8-B reads)
   uint32_t G[20];
-  coded_elements<SGN>(L, b, esh, wlast, es, G);
+#pragma unroll
+  for (int x = 0; x < 10; x++) {
+    const uint2 v = *(const uint2*)(L.IMG + es + 2 * x);
+    G[2 * x] = v.x;
+    G[2 * x + 1] = v.y;
+  }
   uint32_t H[18];
 #pragma unroll
   for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
@@ -501,7 +529,9 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
   const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
   uint32_t xk[16], ae, be;
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  coded_lane<CB, SGN>(L, b, esh, wlast, w, l, x0, x1, xk, ae, be);
+  bwr_materialize<SGN>(L, b, esh, wlast, w, l);
+  lds_barrier();  // the decoded stream
+  coded_lane<CB>(L, w, l, x0, x1, xk, ae, be);
   const uint64_t c4 = prof ? __builtin_amdgcn_s_memtime() : 0;
   lds_barrier();
   // the start state (X, D) of this wave's block: the exclusive fold of the
@@ -534,12 +564,14 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
   lds_barrier();
   const uint64_t c6 = prof ? __builtin_amdgcn_s_memtime() : 0;
   uint8_t* const o = d.out + 16u * T;
+  // value 4096 k + 1024 r + T sits at dword vslot(T) + 4096 k + 1024 r (the
+  // swizzle depends only on bits of T): one base, constant offsets
+  const uint32_t* const vb = L.IMG + vslot(T);
 #pragma unroll
   for (uint32_t r = 0; r < 4; r++) {
-    const uint32_t j = 1024 * r + T;
     uint32_t x[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) x[k] = L.IMG[vslot(4096 * k + j)];
+    for (uint32_t k = 0; k < 4; k++) x[k] = vb[4096 * k + 1024 * r];
     const v4u v = unshuffle4(x);
     if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
       __builtin_nontemporal_store(v, (g_u4*)(o + 16384u * r));
@@ -590,26 +622,48 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
     decline(kp, t);
     return;
   }
-  // the image's aligned cover: every wave moves units 64 (w + 16 i) + l
+  // The image's aligned cover by LDS-DMA.  Wave 0 first moves the prefix
+  // (units [0, PFX): tile and chunk headers, every window header, the frame
+  // and the DD headers -- all the parse reads) and parses as soon as that
+  // has landed, while the rest of the image (units PFX + 64 (w + 16 i) + l,
+  // every wave) is still in flight; one barrier then publishes the landed
+  // image and the parse.
   {
     const uint64_t a0 = (uint64_t)d.in & ~15ull;
     const uint32_t nu = (uint32_t)((((uint64_t)d.in & 15) + d.fs + 15) >> 4);
+    if (w == 0) {
 #pragma unroll
-    for (uint32_t i = 0; i < (IMGU + NT - 1) / NT; i++) {
-      const uint32_t u0 = 64 * (w + 16 * i);
-      if (u0 < nu && u0 + l < nu) dma16(a0 + 16ull * (u0 + l), lds_addr(L.IMG) + 16 * u0);
+      for (uint32_t k = 0; k < PFX / 64; k++)
+        if (64 * k < nu && 64 * k + l < nu) dma16(a0 + 16ull * (64 * k + l), lds_addr(L.IMG) + 1024 * k);
+    }
+    uint32_t after = 0;  // DMA instructions this wave issues after the prefix
+#pragma unroll
+    for (uint32_t i = 0; i < (IMGU - PFX + NT - 1) / NT; i++) {
+      const uint32_t u0 = PFX + 64 * (w + 16 * i);
+      if (u0 < nu) {
+        after++;
+        if (u0 + l < nu) dma16(a0 + 16ull * (u0 + l), lds_addr(L.IMG) + 16 * u0);
+      }
+    }
+    if (w == 0 && ABL != 1) {
+      // (vmcnt counts in issue order: the prefix has landed when at most
+      // `after` of this wave's DMA instructions are left)
+      switch (__builtin_amdgcn_readfirstlane(after)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      }
+      // (the parse is the one serial step of a tile: it issues first on its
+      // SIMD, ahead of the other workgroup's waves)
+      __builtin_amdgcn_s_setprio(3);
+      parse<SGN>(L, d, l, chunked);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
   const uint64_t c1 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  if (w == 0 && ABL != 1) {
-    // (the other waves wait at the barrier: the parse wave issues first on
-    // its SIMD, ahead of the other workgroup's waves)
-    __builtin_amdgcn_s_setprio(3);
-    parse<SGN>(L, d, l, chunked);
-    __builtin_amdgcn_s_setprio(0);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_barrier();
   const uint64_t c2 = prof ? __builtin_amdgcn_s_memtime() : 0;
   if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
