@@ -468,6 +468,18 @@ def variant_line(cfgname, var, r, world):
             "traffic": load_traffic(cfgname, var)}
 
 
+def cgroup_cpus():
+    """The process's CPU quota in CPUs (cgroup v2 cpu.max 'quota period'), or
+    None when unlimited / unreadable.  On the GPU boxes the quota is what a
+    job may use, not the CPUs in its affinity list."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except Exception:
+        return None
+
+
 def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, scaling=False):
     cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
                                 ntiles_sample, threads, seconds)
@@ -478,16 +490,17 @@ def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, 
         "kind": "port",
         "sample": f"{ntl} {cfgname.upper()} '{var}' tiles ({min(ntiles_sample, r['offs'].size)}-tile sample, "
                   f"repeated) in {el:.2f}s on {threads} threads of '{cpu_model()}' ({os.cpu_count()} CPUs "
-                  f"visible, {len(os.sched_getaffinity(0))} in this process's affinity; 16 threads = one GPU's "
-                  "share of the box), tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry, the reference's "
-                  "tile x chunk-range split)",
+                  f"visible, {len(os.sched_getaffinity(0))} in this process's affinity, cgroup quota "
+                  f"{cgroup_cpus() or 'none'} CPUs: the threads used = the quota, every core the job may use), "
+                  "tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry, the reference's tile x chunk-range split)",
+        "cgroup_cpu_quota": cgroup_cpus(),
     }
     if scaling:
         # per-thread rate and the thread-scaling curve of the same sample, so
         # the all-cores figure can be read off (the box lends a GPU job 16
         # threads; running on all of them is not allowed there)
         curve = {}
-        for t in (1, 2, 4, 8):
+        for t in (1, 2, 4, 8, 12):
             if t < threads:
                 v, _, _ = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
                                        min(ntiles_sample, 256 * t), t, max(1.0, seconds / 5))
@@ -677,7 +690,9 @@ def main():
     line = headline_line(args, W, variants, res, world)
     head = min(variants, key=lambda v: gibps(res[v], world))
     r = res[head]
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    # every core the job may use: the cgroup quota (16 on the GPU boxes), not
+    # the affinity list (the whole machine there)
+    threads = args.cpu_threads or min(cgroup_cpus() or 16, len(os.sched_getaffinity(0)))
     if world == 1 and args.others and args.config == "c5" and not args.tiles_per_gpu:
         # every other BASELINE config at its per-GPU size, and C5 at 100k tiles
         others = {}

@@ -447,17 +447,24 @@ __device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh
     const uint32_t kind = te[j].x >> 20;
     ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);  // LDS byte of element e's compressed value
   }
+  // (every round's five dwords first, so that all 20 reads are in flight
+  // together; the decoders below pick from them)
+  uint32_t D[4][5];
 #pragma unroll
   for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t kind = te[j].x >> 20, mn = te[j].y;
+    const uint32_t* p = L.IMG + (ea[j] >> 2);
+#pragma unroll
+    for (int k = 0; k < 5; k++) D[j][k] = p[k];
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
     if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
-      const uint32_t y = rd32(L.IMG, ea[j]);
+      const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
       dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
     } else {
-      const uint32_t* p = L.IMG + (ea[j] >> 2);
-      const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], sh = ea[j] & 3;
-      const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh), r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-      const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh), r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+      const uint32_t r0 = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh), r1 = __builtin_amdgcn_alignbyte(D[j][2], D[j][1], sh);
+      const uint32_t r2 = __builtin_amdgcn_alignbyte(D[j][3], D[j][2], sh), r3 = __builtin_amdgcn_alignbyte(D[j][4], D[j][3], sh);
       const bool b8 = kind == 0, raw = kind == 2;
       // element i: 8-bit -> byte i of r0; 16-bit -> half (i & 1) of r(i >> 1)
       const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
