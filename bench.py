@@ -57,6 +57,9 @@ CONFIGS = {
     "c5": dict(tiles_per_gpu=12500, total_tiles=100000, variants="active,rand,ramp", dtype="int32",
                workload="C5: dense int32, [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)], "
                         "64 KiB tiles (1 chunk), device-resident, 100k tiles sharded over the GPUs"),
+    "c5s": dict(tiles_per_gpu=163840, variants="active,rand,ramp", dtype="int32",
+                workload="C5 pipeline on 40,000-B tiles (10,000 int32 values, one chunk), 163,840 tiles "
+                         "per GPU (the c5 leg's 6.55 GB of output)"),
     "c5big": dict(tiles_per_gpu=200, variants="active", dtype="int32",
                   workload="C5 pipeline, 4 MiB tiles (64 chunks of 64 KiB), 200 tiles per GPU: "
                            "chunk-parallel launch (device chunk directory)"),
@@ -424,11 +427,10 @@ def frac(r):
 
 def kernel_name(cfgname, r):
     if cfgname == "c5big" and r.get("stream_chunks"):
-        return ("chunk directory (dir_count/dir_scan/dir_fill) + unfilter_stream_kernel + unfilter_stream_raw_kernel "
-                "on chunk records + unfilter_fused_kernel (queue of declined chunks)")
-    if cfgname in ("c5", "c5big") and r["streamed"]:
-        return ("unfilter_stream_kernel + unfilter_stream_raw_kernel + unfilter_fused_kernel (queue of "
-                "declined tiles)")
+        return ("chunk directory (dir_count/dir_scan/dir_fill) + unfilter_c5tile_kernel on chunk records + "
+                "unfilter_fused_kernel (queue of declined chunks)")
+    if cfgname in ("c5", "c5s", "c5big") and r["streamed"]:
+        return "unfilter_c5tile_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname == "c1" and r["streamed"]:
         return "unfilter_shuffle4_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname in ("c3a", "c3b", "c4") and r["streamed"]:
@@ -655,6 +657,8 @@ def main():
     ap.add_argument("--no-others", dest="others", action="store_false")
     ap.add_argument("--shard-tiles", type=int, default=12500,
                     help="N = 1 run: also time C5 on one GPU's shard of an 8-GPU node (100k / 8)")
+    ap.add_argument("--c5s-tiles", type=int, default=CONFIGS["c5s"]["tiles_per_gpu"],
+                    help="N = 1 run: also time the C5 pipeline on 40,000-B tiles (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -732,6 +736,20 @@ def main():
                 "tiles": args.shard_tiles, "steps": args.steps, "variants": sh,
                 "min_over_variants_GiBps": round(min(x["GiBps"] for x in sh.values()), 2),
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sh.values()), 4)}
+        # the C5 pipeline on 40,000-B tiles (one chunk of 10,000 values: not
+        # 64 KiB, byte planes not 16-B aligned), the same output bytes
+        if args.c5s_tiles:
+            ss = {}
+            _, cres = run_config(engine, ctx, W, args, "c5s", variants, args.c5s_tiles, args.steps, args.warmup,
+                                 dist, world, rank)
+            for v in variants:
+                ss[v] = variant_line("c5s", v, cres[v], world)
+                cres[v].pop("packed", None)
+            line["config"]["c5_40000B_tiles"] = {
+                "workload": CONFIGS["c5s"]["workload"], "tiles": args.c5s_tiles, "steps": args.steps,
+                "kernel": kernel_name("c5s", cres[variants[0]]), "variants": ss,
+                "min_over_variants_GiBps": round(min(x["GiBps"] for x in ss.values()), 2),
+                "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in ss.values()), 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # after every timed region, at N = 1 only (the N > 1 lines divide the
         # same job over more GPUs; the CPU figure does not change with N)

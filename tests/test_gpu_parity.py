@@ -573,10 +573,10 @@ def test_chunk_parallel_corrupt_mix(eng, ctx, oracle_mod):
 @pytest.mark.parametrize("variant", ["active", "ramp", "rand"])
 def test_chunk_stream_multichunk(eng, ctx, oracle_mod, variant):
     """Multi-chunk C5 tiles (1 MiB minus a few values: 16 chunks, the last
-    one short) in a chunk-parallel launch: the streaming kernels take the
-    full 64 KiB chunks from the device chunk directory (coded-DD for
-    'active', raw-DD for 'ramp'/'rand'), the fused kernel the short last
-    ones; bit-exact vs the oracle, no fallback."""
+    one short) in a chunk-parallel launch: the C5 tile kernel
+    (tdbg_c5tile.hip) takes every chunk from the device chunk directory --
+    the short last ones and the chunks of tiles whose outputs start only
+    4-B aligned included; bit-exact vs the oracle, no fallback."""
     import workloads as W
     from tiledb_amd.filter_pipeline import Datatype
     ser = W.c5_pipeline_bytes()
@@ -595,13 +595,11 @@ def test_chunk_stream_multichunk(eng, ctx, oracle_mod, variant):
     f1, b1, _ = ctx.path_stats()
     assert not st.any()
     assert b1 - b0 == 0 and f1 - f0 == n
-    # every full chunk of a tile whose output starts 16-B aligned (the
-    # streaming kernels' store rule; the outputs here are packed back to
-    # back, and these tiles' sizes are 4 mod 16 apart); the short last ones
-    # and the unaligned tiles' chunks went to the fused kernel
+    # (the outputs are packed back to back and these tiles' sizes are 4 mod
+    # 16 apart: most tiles' chunks start only 4-B aligned)
     aligned = sum(int(batch.out_off[i]) % 16 == 0 for i in range(n))
     assert 0 < aligned < n
-    assert ctx.stream_chunks() - c0 == 15 * aligned
+    assert ctx.stream_chunks() - c0 == 16 * n
     out = batch.outputs_host()
     for i in range(n):
         o = int(batch.out_off[i])

@@ -73,7 +73,7 @@ constexpr uint32_t PFX = 192;         // 16-B units of the image prefix the pars
 struct Lds {
   uint32_t IMG[IMGU * 4];
   uint2 TAB[TABN];  // {image offset of the window's data | kind << 20, window minimum}
-  uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1
+  uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1, Lb, values
   uint32_t red[16][2];  // coded tiles: each wave's DD aggregate (A, B)
 };
 
@@ -88,9 +88,10 @@ __device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
 }
 
 // the tile's shape is one this kernel decodes (descriptor checks only)
+// (a chunk of 4 n bytes, 16 <= n <= 16384 values; the output 4-B aligned)
 __device__ __forceinline__ bool takes(const KParams& kp, const Desc& d) {
-  return !(kp.flags & TDBG_TILE_OFFSETS) && d.os == OUTB && (((uintptr_t)d.out) & 15) == 0 &&
-         d.fs <= IMG_CAP;
+  return !(kp.flags & TDBG_TILE_OFFSETS) && d.os >= 64 && d.os <= OUTB && (d.os & 3) == 0 &&
+         (((uintptr_t)d.out) & 3) == 0 && d.fs <= IMG_CAP;
 }
 
 __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
@@ -146,7 +147,8 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + ho), fl = rd32(P, b + ho + 4),
                  ml = rd32(P, b + ho + 8);
   const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4), ws = rd32(P, m + 13);  // ws: window 0's byte count
-  bool ok = (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= d.fs && nwr >= 2 &&
+  const uint32_t os = (uint32_t)d.os, nv = os >> 2;
+  bool ok = (chunked || (nlo == 1 && nhi == 0)) && orig == os && (uint64_t)ml + fl + ho + 12 <= d.fs && nwr >= 1 &&
             nwr <= TABN && ml == 8 + 9 * nwr + 24 && Lb <= LBWR && Lb >= 34 + 8 && ws >= 256 && ws <= 4096 &&
             (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwr;
   const uint32_t nwin = ok ? nwr : 2;
@@ -188,7 +190,7 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   }
   // ---- round 2: the compression frame md (compression_filter.cc:413-486):
   // 1 md part of 8 B (the byteshuffle header) compressed to 17 B, 1 data part
-  // of 65,536 B compressed to d5 bytes (the BWR output is c0 + c1); the DD
+  // of os bytes compressed to d5 bytes (the BWR output is c0 + c1); the DD
   // headers = BWR-output bytes [0, 34): lane e decodes element e < 9 of
   // window 0
   const uint32_t k0 = __builtin_amdgcn_readfirstlane(kind[0]), mn0 = __builtin_amdgcn_readfirstlane(mn[0]);
@@ -200,19 +202,19 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   v = k0 == 2 ? v : (k0 == 0 ? ext<SGN>(v, 0, 8) : ext<SGN>(v, 0, 16)) + mn0;
   auto fr = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(fv, k); };
   const uint32_t d5 = fr(5);
-  ok = ok && fr(0) == 1 && fr(1) == 1 && fr(2) == 8 && fr(3) == 17 && fr(4) == OUTB && d5 + 17 == Lb;
+  ok = ok && fr(0) == 1 && fr(1) == 1 && fr(2) == 8 && fr(3) == 17 && fr(4) == os && d5 + 17 == Lb;
   auto dw = [&](int k) -> uint32_t { return __builtin_amdgcn_readlane(v, k); };
   auto dd = [&](int o) -> uint32_t { return __builtin_amdgcn_alignbyte(dw((o >> 2) + 1), dw(o >> 2), o & 3); };
-  // c0 = [u8 bitsize][u64 n = 2][1][65536] (any bitsize: two values, or the
-  // same 8 bytes copied raw); c1 = [u8 bitsize][u64 16384] followed by the
-  // raw values (bitsize >= 31, dd_compressor.cc:233-236) or by [x0][x1] and
-  // 16,382 codes of bitsize + 1 bits in u64 words, MSB first (bitsize 1..30,
-  // dd_compressor.cc:314-404)
+  // c0 = [u8 bitsize][u64 n = 2][1][os] (any bitsize: two values, or the
+  // same 8 bytes copied raw); c1 = [u8 bitsize][u64 nv = os / 4] followed by
+  // the raw values (bitsize >= 31, dd_compressor.cc:233-236) or by [x0][x1]
+  // and nv - 2 codes of bitsize + 1 bits in u64 words, MSB first (bitsize
+  // 1..30, dd_compressor.cc:314-404)
   const uint32_t bs = dd(17) & 0xffu;
-  const uint32_t cb = bs + 1, words = ((OUTB / 4 - 2) * cb + 63) / 64;
+  const uint32_t cb = bs + 1, words = ((nv - 2) * cb + 63) / 64;
   const bool raw = bs >= 31;
-  ok = ok && dd(1) == 2 && dd(5) == 0 && dd(9) == 1 && dd(13) == OUTB && dd(18) == OUTB / 4 && dd(22) == 0 &&
-       (raw ? d5 == 9 + OUTB : bs >= 1 && d5 == 17 + 8 * words);
+  ok = ok && dd(1) == 2 && dd(5) == 0 && dd(9) == 1 && dd(13) == os && dd(18) == nv && dd(22) == 0 &&
+       (raw ? d5 == 9 + os : bs >= 1 && d5 == 17 + 8 * words);
   if (l == 0) {
     L.hd[0] = ok ? 1u : 0u;
     L.hd[1] = 31 - __builtin_clz(ws);
@@ -221,6 +223,7 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
     L.hd[4] = dd(26);
     L.hd[5] = dd(30);
     L.hd[6] = Lb;
+    L.hd[7] = nv;
   }
 }
 
@@ -237,7 +240,8 @@ __device__ __forceinline__ v4u unshuffle4(const uint32_t (&x)[4]) {
 
 // The wave's plane ranges: (r, k) = round r (output units 1024 r + 64 w +
 // [0, 64)), plane k = the 256 BWR-output bytes [Q0, Q0 + 256), Q0 = 26 +
-// 16384 k + 4 (1024 r + 64 w).  A range spans at most two windows (windows
+// nv k + 4 (1024 r + 64 w) for a chunk of nv values (byte shift s = Q0 & 3,
+// the same for a plane's every range: 2 when nv is a multiple of 4).  A range spans at most two windows (windows
 // are >= 256 B), W0 and W1; lane i < 16 reads range i = 4 r + k's two table
 // entries once, and the decode takes them back with v_readlane (no per-lane
 // table lookups).  One wave-uniform BWR^-1 decoder per range:
@@ -246,9 +250,9 @@ __device__ __forceinline__ v4u unshuffle4(const uint32_t (&x)[4]) {
 //   8-bit   both 8-bit: the two element bytes at W0's offset + element index
 //           (full 8-bit windows are contiguous too), each plus its window's
 //           minimum;
-//   general (16-bit or mixed windows) the dword = upper half of element e =
-//           Q / 4 and lower half of e + 1 (Q = 2 mod 4), each decoded from
-//           its own window's entry.
+//   general (16-bit or mixed windows) the dword = bytes [s, 4) of element
+//           e = Q / 4 and bytes [0, s) of e + 1, each decoded from its own
+//           window's entry.
 struct Ranges {
   uint32_t x0, x1;  // table words of W0 and W1 ({data offset | kind << 20})
   uint32_t m0, m1;  // their minima
@@ -259,11 +263,16 @@ struct Ranges {
 };
 
 template <bool SGN>
-__device__ __forceinline__ Ranges setup_ranges(const Lds& L, uint32_t b, uint32_t w, uint32_t l, uint32_t wsh) {
+__device__ __forceinline__ Ranges setup_ranges(const Lds& L, uint32_t b, uint32_t w, uint32_t l, uint32_t wsh,
+                                               uint32_t wlast, uint32_t nv) {
   const uint32_t esh = wsh - 2;
   const uint32_t i = l & 15, r = i >> 2, k = i & 3;
-  const uint32_t Q0 = 26 + 16384 * k + 4 * (1024 * r + 64 * w);
-  const uint32_t W0 = Q0 >> wsh, W1 = (Q0 + 255) >> wsh;
+  const uint32_t Q0 = 26 + nv * k + 4 * (1024 * r + 64 * w);
+  // (a range whose units all lie past the chunk is never decoded or stored:
+  // it reads at LDS byte 0; the bytes past the BWR output that the last
+  // range reads decode to values no store takes, from window wlast)
+  const bool valid = 1024 * r + 64 * w < (nv + 3) >> 2;
+  const uint32_t W0 = min(Q0 >> wsh, wlast), W1 = min((Q0 + 255) >> wsh, wlast);
   const uint2 t0 = L.TAB[W0], t1 = L.TAB[W1];
   const uint32_t k0 = t0.x >> 20, k1 = t1.x >> 20;
   const bool raw = k0 == 2 && k1 == 2, b8 = k0 == 0 && k1 == 0;
@@ -278,18 +287,20 @@ __device__ __forceinline__ Ranges setup_ranges(const Lds& L, uint32_t b, uint32_
     const uint32_t y = rd32(L.IMG, (t1.x & OFFM) + b);
     g.s1 = k1 == 2 ? y : (k1 == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + t1.y;
   }
-  g.base = raw ? (t0.x & OFFM) + (Q0 - (W0 << wsh)) + b : (t0.x & OFFM) + ((Q0 >> 2) - (W0 << esh)) + b;
-  g.is8 = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && b8);
-  g.gen = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && !raw && !b8);
+  g.base = !valid ? 0u
+           : raw  ? (t0.x & OFFM) + (Q0 - (W0 << wsh)) + b
+                  : (t0.x & OFFM) + ((Q0 >> 2) - (W0 << esh)) + b;
+  g.is8 = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && valid && b8);
+  g.gen = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && valid && !raw && !b8);
   return g;
 }
 
 // General ranges (16-bit windows, or two windows of different kinds): lane
-// l's dword = the upper half of element e and the lower half of e + 1.  Both
+// l's dword = bytes [s, 4) of element e and bytes [0, s) of e + 1.  Both
 // come from one read at element e's compressed value in its own window (W0's
-// below e1, else W1's; raw: from its byte 2, so the read holds exactly the
-// dword), except for the one lane whose e + 1 is W1's first element: that
-// half is the range's s1.  The v_readlane's are taken before any select (a
+// below e1, else W1's; raw: from its byte s, so the read holds exactly the
+// dword), except for the one lane whose e + 1 is W1's first element: those
+// bytes are the range's s1.  The v_readlane's are taken before any select (a
 // readlane under a lane-dependent condition becomes an exec-masked branch).
 struct GenRange {
   uint32_t x0, x1, m0, m1, e0, e1, s1;
@@ -300,59 +311,81 @@ __device__ __forceinline__ GenRange gen_range(const Ranges& g, uint32_t i) {
                   (uint32_t)__builtin_amdgcn_readlane(g.e0, i), (uint32_t)__builtin_amdgcn_readlane(g.e1, i),
                   (uint32_t)__builtin_amdgcn_readlane(g.s1, i)};
 }
-__device__ __forceinline__ uint32_t gen_addr(const GenRange& q, uint32_t e, uint32_t b) {
+__device__ __forceinline__ uint32_t gen_addr(const GenRange& q, uint32_t e, uint32_t b, uint32_t s) {
   const bool hi = e >= q.e1;
   const uint32_t tx = hi ? q.x1 : q.x0, st = hi ? q.e1 : q.e0, kind = tx >> 20;
-  return (tx & OFFM) + ((e - st) << kind) + b + (kind == 2 ? 2u : 0u);
+  return (tx & OFFM) + ((e - st) << kind) + b + (kind == 2 ? s : 0u);
 }
 template <bool SGN>
-__device__ __forceinline__ uint32_t gen_dword(const GenRange& q, uint32_t e, uint32_t y) {
+__device__ __forceinline__ uint32_t gen_dword(const GenRange& q, uint32_t e, uint32_t y, uint32_t s) {
   const bool hi = e >= q.e1;
   const uint32_t tx = hi ? q.x1 : q.x0, mn = hi ? q.m1 : q.m0, kind = tx >> 20;
   const uint32_t v0 = (kind == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + mn;
   const uint32_t v1 = (kind == 0 ? ext<SGN>(y, 8, 8) : ext<SGN>(y, 16, 16)) + mn;
-  const uint32_t a = kind == 2 ? y : v0 >> 16;
-  const uint32_t bn = kind == 2 ? y >> 16 : v1;
+  // raw: y = the dword itself (bytes [s, 4) of e, then e + 1's); as values:
+  // e's at its bytes [s, 4), e + 1's at [0, s)
+  const uint32_t a = kind == 2 ? y << (8 * s) : v0;
+  const uint32_t bn = kind == 2 ? __builtin_amdgcn_alignbyte(0u, y, 4 - s) : v1;
   const uint32_t bh = e + 1 == q.e1 ? q.s1 : bn;
-  return __builtin_amdgcn_perm(bh, a, 0x05040100u);
+  return __builtin_amdgcn_alignbyte(bh, a, s);
+}
+
+// Output unit u (16 B at o + 16384 r, u = 1024 r + T) of a chunk of nv
+// values: whole below nv / 4, the last one partial (nv mod 4 dwords) when
+// nv is not a multiple of 4, nothing past it.  The output is 4-B aligned
+// (a chunk of a multi-chunk tile starts at a multiple of its size).
+typedef uint32_t v4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) v4a g_a4;
+__device__ __forceinline__ void store_unit(uint8_t* p, const v4u& v, uint32_t u, uint32_t nv) {
+  if (u < (nv >> 2)) {
+    __builtin_nontemporal_store((v4a)v, (g_a4*)p);
+  } else if (u < ((nv + 3) >> 2)) {
+    uint32_t* q = (uint32_t*)p;
+    q[0] = v.x;
+    if ((nv & 3) > 1) q[1] = v.y;
+    if ((nv & 3) > 2) q[2] = v.z;
+  }
 }
 
 // NR ranges (NR / 4 rounds from round r0): reads, decode, stores
 template <bool SGN, int ABL, bool GEN, int NR>
 __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint32_t b, uint32_t w, uint32_t l,
-                                             uint8_t* o, uint32_t r0) {
+                                             uint8_t* o, uint32_t r0, uint32_t nv) {
   uint32_t y[NR];
 #pragma unroll
   for (uint32_t j = 0; j < NR; j++) {
     const uint32_t i = 4 * r0 + j;
-    const uint32_t e = ((26 + 16384 * (i & 3) + 4 * (1024 * (i >> 2) + 64 * w)) >> 2) + l;
+    const uint32_t Q0 = 26 + nv * (i & 3) + 4 * (1024 * (i >> 2) + 64 * w);
+    const uint32_t e = (Q0 >> 2) + l;
     uint32_t a = __builtin_amdgcn_readlane(g.base, i) + (((g.is8 >> i) & 1) ? l : 4 * l);
-    if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b);
+    if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b, Q0 & 3);
     y[j] = (ABL == 1 || ABL == 2) ? l + i : rd32(L.IMG, a);
   }
 #pragma unroll
   for (uint32_t rr = 0; rr < NR / 4; rr++) {
     const uint32_t r = r0 + rr;
+    if (1024 * r + 64 * w >= ((nv + 3) >> 2)) break;  // (wave-uniform: no unit of this round is in the chunk)
     uint32_t x[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
       const uint32_t i = 4 * r + k;
       x[k] = y[4 * rr + k];
       if (ABL == 1 || ABL == 2 || ABL == 5) continue;
-      const uint32_t e = ((26 + 16384 * k + 4 * (1024 * r + 64 * w)) >> 2) + l;
+      const uint32_t Q0 = 26 + nv * k + 4 * (1024 * r + 64 * w);
+      const uint32_t e = (Q0 >> 2) + l, sk = Q0 & 3;
       // (wave-uniform branches: all 16 reads are already in flight)
       if ((g.is8 >> i) & 1) {
         const uint32_t m0 = __builtin_amdgcn_readlane(g.m0, i), m1 = __builtin_amdgcn_readlane(g.m1, i),
                        e1 = __builtin_amdgcn_readlane(g.e1, i);
         const uint32_t v0 = ext<SGN>(x[k], 0, 8) + (e < e1 ? m0 : m1), v1 = ext<SGN>(x[k], 8, 8) + (e + 1 < e1 ? m0 : m1);
-        x[k] = __builtin_amdgcn_perm(v1, v0, 0x05040302u);
+        x[k] = __builtin_amdgcn_alignbyte(v1, v0, sk);
       } else if (GEN && ((g.gen >> i) & 1)) {
-        x[k] = gen_dword<SGN>(gen_range(g, i), e, x[k]);
+        x[k] = gen_dword<SGN>(gen_range(g, i), e, x[k], sk);
       }
     }
     const v4u v = unshuffle4(x);
     if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
-      __builtin_nontemporal_store(v, (g_u4*)(o + 16384u * r));
+      store_unit(o + 16384u * r, v, 1024 * r + 64 * w + l, nv);
   }
 }
 
@@ -532,7 +565,7 @@ __device__ __forceinline__ uint32_t vslot(uint32_t v) {
 // values into LDS (second barrier), then byteshuffle^-1 and the stores.
 template <int CB, bool SGN, int ABL>
 __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, uint32_t esh, uint32_t wlast,
-                                           uint32_t w, uint32_t l, uint64_t* prof) {
+                                           uint32_t w, uint32_t l, uint32_t nv, uint64_t* prof) {
   const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
   uint32_t xk[16], ae, be;
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -571,17 +604,35 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
   lds_barrier();
   const uint64_t c6 = prof ? __builtin_amdgcn_s_memtime() : 0;
   uint8_t* const o = d.out + 16u * T;
-  // value 4096 k + 1024 r + T sits at dword vslot(T) + 4096 k + 1024 r (the
-  // swizzle depends only on bits of T): one base, constant offsets
-  const uint32_t* const vb = L.IMG + vslot(T);
+  if (nv == OUTB / 4) {
+    // value 4096 k + 1024 r + T sits at dword vslot(T) + 4096 k + 1024 r (the
+    // swizzle depends only on bits of T): one base, constant offsets
+    const uint32_t* const vb = L.IMG + vslot(T);
 #pragma unroll
-  for (uint32_t r = 0; r < 4; r++) {
-    uint32_t x[4];
+    for (uint32_t r = 0; r < 4; r++) {
+      uint32_t x[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) x[k] = vb[4096 * k + 1024 * r];
-    const v4u v = unshuffle4(x);
-    if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
-      __builtin_nontemporal_store(v, (g_u4*)(o + 16384u * r));
+      for (uint32_t k = 0; k < 4; k++) x[k] = vb[4096 * k + 1024 * r];
+      const v4u v = unshuffle4(x);
+      if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
+        __builtin_nontemporal_store((v4a)v, (g_a4*)(o + 16384u * r));
+    }
+  } else {
+    // nv values: plane k starts at stream byte nv k, so unit u's plane dword
+    // is bytes [nv k + 4 u, + 4) of the value stream (two values when nv k is
+    // not a multiple of 4)
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      if (1024 * r + 64 * w >= ((nv + 3) >> 2)) break;  // (wave-uniform)
+      uint32_t x[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t v0 = ((nv * k) >> 2) + 1024 * r + T;
+        x[k] = __builtin_amdgcn_alignbyte(L.IMG[vslot(v0 + 1)], L.IMG[vslot(v0)], (nv * k) & 3);
+      }
+      const v4u v = unshuffle4(x);
+      store_unit(o + 16384u * r, v, 1024 * r + T, nv);
+    }
   }
   if (prof && l == 0 && (w == 0 || w == 15)) {
     // coded tiles: 2 codes + wave scan, 3 B3 + fold + value writes, 4 B4,
@@ -680,12 +731,13 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
   const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
   const uint32_t cb = __builtin_amdgcn_readfirstlane(L.hd[3]);
+  const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
+  const uint32_t nv = __builtin_amdgcn_readfirstlane(L.hd[7]);
   if (cb != 0) {
     // coded DoubleDelta: one instantiation per code width
-    const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
     switch (cb) {
 #define TDBG_CB(c) \
-  case c: coded_tile<c, SGN, ABL>(L, d, b, wsh - 2, wlast, w, l, prof); break;
+  case c: coded_tile<c, SGN, ABL>(L, d, b, wsh - 2, wlast, w, l, nv, prof); break;
       TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
       TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
       TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
@@ -706,14 +758,14 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
           atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_CHUNKS], 1ull);
         } else {
           atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
-          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)d.os);
           atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
         }
       }
     }
     return;
   }
-  const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh);
+  const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh, wlast, nv);
   uint8_t* const o = d.out + 16u * (64 * w + l);
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
   // All 16 ranges' reads first, then the decode and one store per round.
@@ -723,13 +775,13 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   // access, so the reads stay in flight together (8 at a time in such waves,
   // for registers).
   if (g.gen == 0 || ABL == 4) {
-    decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0);
+    decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
   } else if (ABL == 6) {
-    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0);
-    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2);
+    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
+    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv);
   } else {
-    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0);
-    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2);
+    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0, nv);
+    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2, nv);
   }
   if (prof && l == 0) {
     const uint64_t c4 = __builtin_amdgcn_s_memtime();
@@ -754,7 +806,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_CHUNKS], 1ull);
       } else {
         atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
-        atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+        atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)d.os);
         atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
         atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_RAW_TILES], 1ull);
       }

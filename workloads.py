@@ -21,6 +21,7 @@ import numpy as np
 
 TILE_VALUES = 16384          # 64 KiB of int32 per tile (one 64 KiB chunk)
 TILE_BYTES = TILE_VALUES * 4
+C5S_VALUES = 10000           # bench.py --config c5s: 40,000-B tiles
 
 
 def _dd_int32(v: np.ndarray) -> bytes:
@@ -340,6 +341,10 @@ def config(name: str):
         "c4": (P(PositiveDeltaFilter(1024), BitWidthReductionFilter(256)), Datatype.UINT64, 8,
                lambda var, k, rng: c4_values(k, rng), c4_tile),
         "c5": (c5_pipeline_bytes(), Datatype.INT32, 4, c5_values, c5_filter_tile),
+        # C5's pipeline over 40,000-B tiles (10,000 values: one chunk that is
+        # not 64 KiB, planes not 16-B aligned in the BWR output)
+        "c5s": (c5_pipeline_bytes(), Datatype.INT32, 4,
+                lambda var, k, rng: c5_values(var, k, rng, C5S_VALUES), c5_filter_tile),
         # C5's pipeline over 4 MiB tiles (64 chunks of 64 KiB): the chunk-
         # parallel launch (device chunk directory) against tile-serial chunks
         "c5big": (c5_pipeline_bytes(), Datatype.INT32, 4,
@@ -382,8 +387,8 @@ def pool(name: str, variant: str, nunique: int, seed: int, encode=None):
     return [tile(v) for v in vals], vals
 
 
-def c5_values(variant: str, tile_index: int, rng: np.random.Generator) -> np.ndarray:
-    """C5 tile values.
+def c5_values(variant: str, tile_index: int, rng: np.random.Generator, n: int = TILE_VALUES) -> np.ndarray:
+    """C5 tile values (n of them: 16,384 for a 64 KiB tile).
     rand:   uniform int32; every byte moves, DD falls back to raw and every BWR
             window is raw (two stages are views).
     ramp:   a = tile*16384 + i; DD raw (bitsize 33 >= 31), half the BWR windows
@@ -393,16 +398,16 @@ def c5_values(variant: str, tile_index: int, rng: np.random.Generator) -> np.nda
             (< 31: the bit-packed path), ~92 % of the BWR windows over DD's
             output 8-bit, byteshuffle over the whole tile (~20 KB filtered)."""
     if variant == "ramp":
-        return (np.arange(TILE_VALUES, dtype=np.int64) + tile_index * TILE_VALUES).astype(np.int32)
+        return (np.arange(n, dtype=np.int64) + tile_index * n).astype(np.int32)
     if variant == "rand":
-        return rng.integers(-2**31, 2**31, TILE_VALUES, dtype=np.int64).astype(np.int32)
+        return rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
     if variant == "active":
-        out = np.empty(TILE_VALUES, dtype=np.int32)
+        out = np.empty(n, dtype=np.int32)
         i = 0
-        while i < TILE_VALUES:
-            n = int(rng.integers(256, 2048))
-            out[i:i + n] = rng.integers(0, 16)
-            i += n
+        while i < n:
+            run = int(rng.integers(256, 2048))
+            out[i:i + run] = rng.integers(0, 16)
+            i += run
         return out
     raise ValueError(variant)
 
