@@ -392,6 +392,28 @@ def test_shuffle4_declined_tiles(eng, ctx, oracle_mod):
     assert ctx.stream_tiles() == s0
 
 
+def test_shuffle4_every_tile_size(eng, ctx, oracle_mod):
+    """One-chunk [BYTESHUFFLE] int32 / uint32 tiles of every size class up to
+    64 KiB (n = 4 .. 16,384 values, n mod 4 = 0..3: planes at every byte
+    alignment, a partial last unit), mixed back to back (outputs 4-B
+    aligned): every tile taken by the unit-parallel kernel, bit-exact."""
+    from tests.test_gpu_parity import check_parity_replicated, encode
+    from tiledb_amd.filter_pipeline import ByteshuffleFilter
+    rng = np.random.default_rng(65)
+    sizes = [16, 20, 24, 28, 1000, 4004, 4008, 4012, 40000, 40004, 65520, 65524, 65528, 65532, 65536]
+    for dt, npt in ((Datatype.INT32, np.int32), (Datatype.UINT32, np.uint32)):
+        tiles = [as_u8(rng.integers(-2**31, 2**31, nb // 4, dtype=np.int64).astype(npt)) for nb in sizes]
+        case = Case("c1_sizes", P(ByteshuffleFilter()), dt, 4, tiles)
+        _, enc = encode(oracle_mod, case)
+        assert len(enc) == len(sizes)
+        f0, b0, _ = ctx.path_stats()
+        s0 = ctx.stream_tiles()
+        check_parity_replicated(eng, ctx, oracle_mod, case, enc, 330)
+        f1, b1, _ = ctx.path_stats()
+        assert b1 - b0 == 0 and f1 - f0 == 330
+        assert ctx.stream_tiles() - s0 == 330
+
+
 @pytest.mark.parametrize("cfg", ["c3a", "c3b", "c4"])
 def test_small_chunk_stream_multichunk(eng, ctx, oracle_mod, cfg):
     """Multi-chunk C3a / C3b / C4 tiles (16 chunks of 8,192 u64 values, the

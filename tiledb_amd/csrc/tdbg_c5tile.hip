@@ -467,7 +467,7 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
 // barrier after which the decoded units overwrite the image.
 template <bool SGN>
 __device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w,
-                                                uint32_t l) {
+                                                uint32_t l, uint32_t nun) {
   v4u dv[4];
   uint2 te[4];
   uint32_t ea[4];
@@ -482,15 +482,19 @@ __device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh
   }
   // (every round's five dwords first, so that all 20 reads are in flight
   // together; the decoders below pick from them)
+  // (rounds whose units all lie past the BWR output, nun units, are skipped:
+  // a wave-uniform test)
   uint32_t D[4][5];
 #pragma unroll
   for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
     const uint32_t* p = L.IMG + (ea[j] >> 2);
 #pragma unroll
     for (int k = 0; k < 5; k++) D[j][k] = p[k];
   }
 #pragma unroll
   for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
     const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
     if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
       const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
@@ -509,14 +513,29 @@ __device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh
   }
   lds_barrier();  // every compressed byte is in registers: the stream may overwrite the image
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+  for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
+    *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+  }
 }
 
 // The lane's 16 values (local running sums) and its exclusive wave prefix
 // (ae, be); lane 63 publishes the wave total.
 template <int CB>
 __device__ __forceinline__ void coded_lane(Lds& L, uint32_t w, uint32_t l, uint32_t x0, uint32_t x1,
-                                           uint32_t (&xk)[16], uint32_t& ae, uint32_t& be) {
+                                           uint32_t (&xk)[16], uint32_t& ae, uint32_t& be, uint32_t nv) {
+  if (1024 * w >= nv) {
+    // (a wave whose values all lie past the chunk: nothing to decode; its
+    // block folds as zeros, after every real value)
+#pragma unroll
+    for (int i = 0; i < 16; i++) xk[i] = 0;
+    ae = be = 0;
+    if (l == 63) {
+      L.red[w][0] = 0;
+      L.red[w][1] = 0;
+    }
+    return;
+  }
   const int32_t T = (int32_t)(64 * w + l);
   const int32_t P0 = (16 * T - 2) * CB;  // stream bit of the lane's first code
   const int32_t b0 = (P0 + 31) >> 5;
@@ -569,9 +588,9 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
   const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
   uint32_t xk[16], ae, be;
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  bwr_materialize<SGN>(L, b, esh, wlast, w, l);
+  bwr_materialize<SGN>(L, b, esh, wlast, w, l, (__builtin_amdgcn_readfirstlane(L.hd[6]) + 15) >> 4);
   lds_barrier();  // the decoded stream
-  coded_lane<CB>(L, w, l, x0, x1, xk, ae, be);
+  coded_lane<CB>(L, w, l, x0, x1, xk, ae, be, nv);
   const uint64_t c4 = prof ? __builtin_amdgcn_s_memtime() : 0;
   lds_barrier();
   // the start state (X, D) of this wave's block: the exclusive fold of the
@@ -628,7 +647,10 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) {
         const uint32_t v0 = ((nv * k) >> 2) + 1024 * r + T;
-        x[k] = __builtin_amdgcn_alignbyte(L.IMG[vslot(v0 + 1)], L.IMG[vslot(v0)], (nv * k) & 3);
+        if ((nv & 3) == 0)
+          x[k] = L.IMG[vslot(v0)];
+        else
+          x[k] = __builtin_amdgcn_alignbyte(L.IMG[vslot(v0 + 1)], L.IMG[vslot(v0)], (nv * k) & 3);
       }
       const v4u v = unshuffle4(x);
       store_unit(o + 16384u * r, v, 1024 * r + T, nv);

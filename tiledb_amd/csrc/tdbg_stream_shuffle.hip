@@ -12,11 +12,15 @@
 // workgroup per tile, so it is no longer bound by one workgroup's latency
 // chain.
 //
-// Each workgroup checks its tile's header (Tile::load_chunk_data,
-// tile.cc:280-313; the byteshuffle metadata [u32 1][u32 65536]); a tile of
-// any other shape is queued by its first workgroup for the fused kernel,
-// which runs on the queue right after, so statuses and bytes stay the
-// reference's.  A workgroup writes only when the whole header validated.
+// Any one-chunk tile of 4 n bytes (n <= 16,384 values: every tile of at
+// most 64 KiB is one chunk, tile.cc:87-100) is taken: plane k starts at
+// data byte k n (any alignment), the last unit is partial when n is not a
+// multiple of 4, and outputs need only be 4-B aligned.  Each workgroup checks
+// its tile's header (Tile::load_chunk_data, tile.cc:280-313; the byteshuffle
+// metadata [u32 1][u32 4 n]); a tile of any other shape is queued by its
+// first workgroup for the fused kernel, which runs on the queue right after,
+// so statuses and bytes stay the reference's.  A workgroup writes only when
+// the whole header validated.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,7 +36,8 @@ constexpr uint32_t OUTB = 65536;
 constexpr uint32_t PARTS = OUTB / 16 / NT;  // workgroups per tile (16)
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) v4u g_u4;
+typedef uint32_t v4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) v4a g_a4;
 typedef __attribute__((address_space(1))) const uint32_t g_cu32;
 
 // bytes [p, p + 4) at any alignment, from the dwords that hold them (only
@@ -54,14 +59,14 @@ __global__ void __launch_bounds__(NT) unfilter_shuffle4_kernel(const KParams kp)
   const uint8_t* in = kp.in[t];
   uint8_t* out = kp.out[t];
   const uint64_t fs = kp.in_size[t], os = kp.out_size[t];
-  bool ok = !(kp.flags & TDBG_TILE_OFFSETS) && os == OUTB && (((uintptr_t)out) & 15) == 0 &&
-            fs >= 28 + OUTB;
+  bool ok = !(kp.flags & TDBG_TILE_OFFSETS) && os >= 16 && os <= OUTB && (os & 3) == 0 &&
+            (((uintptr_t)out) & 3) == 0 && fs >= 28 + os;
   if (ok) {
-    // [u64 nchunks = 1][u32 orig][u32 filtered][u32 md][md = u32 1, u32 65536]
-    // (uniform loads; the image holds at least 28 + 65,536 bytes)
+    // [u64 nchunks = 1][u32 orig][u32 filtered][u32 md][md = u32 1, u32 os]
+    // (uniform loads; the image holds at least 28 + os bytes)
     const uint32_t nlo = ld32u(in), nhi = ld32u(in + 4), orig = ld32u(in + 8), fl = ld32u(in + 12),
                    ml = ld32u(in + 16), np = ld32u(in + 20), ps = ld32u(in + 24);
-    ok = nlo == 1 && nhi == 0 && orig == OUTB && fl == OUTB && ml == 8 && np == 1 && ps == OUTB &&
+    ok = nlo == 1 && nhi == 0 && orig == os && fl == os && ml == 8 && np == 1 && ps == os &&
          (uint64_t)20 + ml + fl <= fs;
   }
   if (!ok) {
@@ -72,9 +77,25 @@ __global__ void __launch_bounds__(NT) unfilter_shuffle4_kernel(const KParams kp)
     }
     return;
   }
+  const uint32_t n = (uint32_t)os >> 2;       // values
   const uint32_t j = part * NT + threadIdx.x;  // output unit
+  if (j >= (n + 3) >> 2) return;
   const uint8_t* d = in + 28 + 4 * j;
-  const uint32_t p0 = ld32u(d), p1 = ld32u(d + 16384), p2 = ld32u(d + 32768), p3 = ld32u(d + 49152);
+  uint32_t p0, p1, p2, p3;
+  if (j < (n >> 2)) {
+    p0 = ld32u(d), p1 = ld32u(d + n), p2 = ld32u(d + 2 * n), p3 = ld32u(d + 3 * n);
+  } else {
+    // the partial last unit: only the planes' n mod 4 remaining bytes (no
+    // read past the tile image)
+    const uint32_t r = n & 3;
+    auto part_ld = [&](const uint8_t* q) -> uint32_t {
+      uint32_t v = q[0];
+      if (r > 1) v |= (uint32_t)q[1] << 8;
+      if (r > 2) v |= (uint32_t)q[2] << 16;
+      return v;
+    };
+    p0 = part_ld(d), p1 = part_ld(d + n), p2 = part_ld(d + 2 * n), p3 = part_ld(d + 3 * n);
+  }
   // out dword b byte k = plane k byte b
   const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
   const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
@@ -82,12 +103,19 @@ __global__ void __launch_bounds__(NT) unfilter_shuffle4_kernel(const KParams kp)
   const uint32_t e = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
   const v4u y{__builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(b, a, 0x07060302u),
               __builtin_amdgcn_perm(e, c, 0x05040100u), __builtin_amdgcn_perm(e, c, 0x07060302u)};
-  __builtin_nontemporal_store(y, (g_u4*)(out + 16 * j));
+  if (j < (n >> 2)) {
+    __builtin_nontemporal_store((v4a)y, (g_a4*)(out + 16 * j));
+  } else {
+    uint32_t* q = (uint32_t*)(out + 16 * j);
+    q[0] = y.x;
+    if ((n & 3) > 1) q[1] = y.y;
+    if ((n & 3) > 2) q[2] = y.z;
+  }
   if (part == 0 && threadIdx.x == 0) {
     if (kp.status) kp.status[t] = TDBG_OK;
     if (kp.stats) {
       atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], 1ull);
-      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+      atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)os);
       atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], 1ull);
     }
   }

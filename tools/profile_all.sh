@@ -4,7 +4,7 @@
 # variant) a rocprofv3 --kernel-trace --stats pass and separate --pmc
 # FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md "HBM"); summary ->
 # gpurun_out/prof_<tag>/summary.json
-# usage: bash tools/profile_all.sh <tag> [configs...]
+# usage: bash tools/profile_all.sh <tag> [configs...]   (BARGS: the bench line's extra arguments)
 set -o pipefail
 TAG=${1:-x}; shift
 CFGS=${@:-"c5 c1 c2 c2i c3a c3b c4"}
@@ -13,9 +13,9 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin" [c5big]="active")
+declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin" [c5big]="active" [c5s]="active rand ramp")
 for CFG in $CFGS; do
-  timeout -k 10 200 python3 -u bench.py --config $CFG --cpu-seconds 5 > $OUT/bench_$CFG.log 2>&1 || { echo "bench $CFG failed"; tail -20 $OUT/bench_$CFG.log; exit 11; }
+  timeout -k 10 200 python3 -u bench.py --config $CFG ${BARGS:---cpu-seconds 5} > $OUT/bench_$CFG.log 2>&1 || { echo "bench $CFG failed"; tail -20 $OUT/bench_$CFG.log; exit 11; }
   tail -1 $OUT/bench_$CFG.log
   for V in ${VARS[$CFG]}; do
     B="$R/bench.py --config $CFG --variants $V --no-cpu-baseline --no-e2e --no-others --no-forward"

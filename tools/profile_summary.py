@@ -1,5 +1,5 @@
 """Summary of tools/profile_all.sh: per (config, variant) the unfilter kernels'
-(streaming kernels + fused on their queue for C3/C4/C5, else fused) rocprofv3 kernel-trace average over the timed launches, per-launch HBM
+(streaming kernels -- C5: the tile kernel -- + fused on their queue for C3/C4/C5, else fused) rocprofv3 kernel-trace average over the timed launches, per-launch HBM
 traffic from the --pmc passes (KiB -> bytes; FETCH_SIZE doubled for gfx950
 16-B/lane streaming reads, MI355X_MICROARCH.md "HBM"), the algorithmic bytes
 and roofline fraction from the bench line of the same workload."""
@@ -13,8 +13,8 @@ import sys
 PEAK = 8000.0
 
 
-KERNELS = ("unfilter_stream", "unfilter_shuffle4", "unfilter_fused_kernel")
-STARTS = ("unfilter_stream_kernel", "unfilter_stream_small_kernel", "unfilter_shuffle4_kernel")
+KERNELS = ("unfilter_stream", "unfilter_c5tile", "unfilter_shuffle4", "unfilter_fused_kernel")
+STARTS = ("unfilter_stream_kernel", "unfilter_c5tile_kernel", "unfilter_stream_small_kernel", "unfilter_shuffle4_kernel")
 
 
 def _launches(items):
