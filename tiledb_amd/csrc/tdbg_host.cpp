@@ -852,7 +852,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     kf.tile_list = c->d_sq + 1;
     kf.ntiles_dev = c->d_sq;
     if (te) tdbg::ev_arm.stop = te[1];  // kernel time = the streaming kernels + the fused one
-    if (!skip_fused) e = tdbg_launch_fast(&kf, grid, stream);
+    static const int qgrid = tdbg_hook_int("TDBG_QGRID", 0);  // experiments: the fused grid on the queue
+    if (!skip_fused) e = tdbg_launch_fast(&kf, qgrid > 0 ? std::min<uint32_t>(grid, (uint32_t)qgrid) : grid, stream);
   } else {
     if (te) tdbg::ev_arm.stop = te[1];
     if (!skip_fused) e = fast ? tdbg_launch_fast(&kp, grid, stream) : tdbg_launch_general(&kp, grid, stream);
@@ -869,7 +870,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     // After a streamed launch (tiles or chunk records) the queue holds only
     // tiles both fast kernels declined (malformed or unusual ones): a small
     // grid, whose dispatch is most of an empty fixup launch's cost
-    const uint32_t fgrid = std::min<uint32_t>(ggrid, (streamed || chunk_stream) ? 32u : (uint32_t)c->cus);
+    static const int fxgrid = tdbg_hook_int("TDBG_FIXUP_GRID", 32);  // experiments
+    const uint32_t fgrid = std::min<uint32_t>(ggrid, (streamed || chunk_stream) ? (uint32_t)fxgrid : (uint32_t)c->cus);
     if (te) tdbg::ev_arm.stop = te[2];
     e = tdbg_launch_fixup(&g, fgrid, stream);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("fixup launch: ") + hipGetErrorString(e));
