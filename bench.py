@@ -482,9 +482,63 @@ def cgroup_cpus():
         return None
 
 
+def _cpulist(path):
+    """'0-7,16,18-19' -> [0..7, 16, 18, 19]; None if unreadable."""
+    try:
+        out = []
+        for part in open(path).read().strip().split(","):
+            a, _, b = part.partition("-")
+            out += list(range(int(a), int(b or a) + 1))
+        return out
+    except Exception:
+        return None
+
+
+def spread_cpus(threads):
+    """`threads` physical cores of NUMA node 0 within this process's
+    affinity, dealt round-robin over the node's L3 domains (CCDs), or None.
+    On the GPU host (2 x EPYC 9575F, 8-core CCDs) the CPU entry's rate is
+    bound by each CCD's memory link (8 threads on one CCD: 38.8 GiB/s, on
+    two: 47.4, 16 threads over four: 51.4; profiles/r05/cpu_curve.txt), so
+    the baseline spreads its threads."""
+    aff = os.sched_getaffinity(0)
+    node0 = _cpulist("/sys/devices/system/node/node0/cpulist") or sorted(aff)
+    groups = {}
+    for c in node0:
+        if c not in aff:
+            continue
+        sib = _cpulist(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") or [c]
+        if min(sib) != c:
+            continue  # an SMT sibling
+        l3 = _cpulist(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") or [0]
+        groups.setdefault(min(l3), []).append(c)
+    order, k = [], 0
+    lists = [groups[g] for g in sorted(groups)]
+    while len(order) < threads and any(k < len(g) for g in lists):
+        order += [g[k] for g in lists if k < len(g)]
+        k += 1
+    return order[:threads] if len(order) >= threads else None
+
+
+def cpu_timed(engine, dp, r, threads, ntiles_sample, seconds):
+    """cpu_baseline with the threads on spread_cpus (the sample copied while
+    pinned, so its pages sit on that node); the affinity is restored."""
+    old = os.sched_getaffinity(0)
+    cpus = spread_cpus(threads)
+    try:
+        packed = r["packed"]
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+            n = min(ntiles_sample, r["offs"].size)
+            packed = packed[: int(r["offs"][n - 1] + r["sizes"][n - 1])].copy()
+        v = cpu_baseline(engine, dp, packed, r["offs"], r["sizes"], r["out_bytes"], ntiles_sample, threads, seconds)
+    finally:
+        os.sched_setaffinity(0, old)
+    return v, cpus
+
+
 def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, scaling=False):
-    cpu, ntl, el = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
-                                ntiles_sample, threads, seconds)
+    (cpu, ntl, el), cpus = cpu_timed(engine, dp, r, threads, ntiles_sample, seconds)
     line = {
         "value": round(cpu, 3),
         "unit": "GiB/s",
@@ -496,6 +550,8 @@ def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, 
                   f"{cgroup_cpus() or 'none'} CPUs: the threads used = the quota, every core the job may use), "
                   "tdbg_unfilter_tiles_cpu (the C-ABI's C++ CPU entry, the reference's tile x chunk-range split)",
         "cgroup_cpu_quota": cgroup_cpus(),
+        "thread_placement": (f"pinned to physical cores {cpus} of NUMA node 0, round-robin over its L3 domains "
+                             "(sample pages first-touched there)") if cpus else "unpinned",
     }
     if scaling:
         # per-thread rate and the thread-scaling curve of the same sample, so
@@ -504,8 +560,7 @@ def cpu_line(engine, dp, r, cfgname, var, threads, seconds, ntiles_sample=2048, 
         curve = {}
         for t in (1, 2, 4, 8, 12):
             if t < threads:
-                v, _, _ = cpu_baseline(engine, dp, r["packed"], r["offs"], r["sizes"], r["out_bytes"],
-                                       min(ntiles_sample, 256 * t), t, max(1.0, seconds / 5))
+                (v, _, _), _ = cpu_timed(engine, dp, r, t, min(ntiles_sample, 256 * t), max(1.0, seconds / 5))
                 curve[str(t)] = round(v, 3)
         curve[str(threads)] = round(cpu, 3)
         line["thread_scaling_GiBps"] = curve
