@@ -107,8 +107,34 @@ def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, devic
         for i, o in zip(idx, offs):
             packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
     out_sizes = [vals[i].nbytes for i in idx]
-    batch = engine.TileBatch.from_packed(packed, offs, sizes, out_sizes, device=device)
+    batch = engine.TileBatch.from_packed(packed, offs, sizes, out_sizes, device=device,
+                                         arena=bench_arena(engine, packed.size, int(sum(out_sizes)), device),
+                                         in_first=bool(int(os.environ.get("TDBG_BENCH_IN_FIRST", "0"))),
+                                         gap=int(os.environ.get("TDBG_BENCH_GAP", "0")))
     return batch, pool, vals, idx, packed, offs, sizes
+
+
+_ARENA = None
+
+
+def bench_arena(engine, in_bytes: int, out_bytes: int, device: int):
+    """One device arena for every timed batch of the run (outputs first, the
+    filtered tiles after them): each leg's tiles sit on the same device pages
+    whatever ran before.  With a fresh allocation per leg, a variant's rate
+    depended on the legs before it (C5 ramp 0.667 first vs 0.693 after rand,
+    rand 0.734 first vs 0.775 after ramp, same kernel and tiles) while the
+    address-translation misses (~1e3 per launch) and the DRAM read requests
+    stayed the same (profiles/r05/order_pmc.txt): the buffers' physical
+    placement, not the TLB.  Grown (reallocated) only when a bigger batch
+    comes; the default run's first batch (C5, 100,000 tiles) is the biggest."""
+    global _ARENA
+    import torch
+    need = engine.TileBatch.arena_bytes(in_bytes, out_bytes) + int(os.environ.get("TDBG_BENCH_GAP", "0"))
+    if _ARENA is None or _ARENA.numel() < need or _ARENA.device.index != device:
+        _ARENA = None
+        torch.cuda.empty_cache()
+        _ARENA = torch.empty(need, dtype=torch.uint8, device=torch.device("cuda", device))
+    return _ARENA
 
 
 def verify(batch, vals, idx) -> None:
@@ -742,6 +768,10 @@ def main():
     else:
         ntiles = cfg["tiles_per_gpu"]
     ctx = engine.Context(torch.cuda.current_device())  # this rank's GPU (set above)
+    # the run's one device arena, sized up front for the config's biggest
+    # variant (C5 rand: 68,003-B images + 64 KiB outputs per tile)
+    tb = W.TILE_BYTES * (64 if args.config == "c5big" else 1)
+    bench_arena(engine, int(ntiles * tb * 1.04), ntiles * tb, torch.cuda.current_device())
     variants = [v for v in (args.variants or cfg["variants"]).split(",") if v]
     dp, res = run_config(engine, ctx, W, args, args.config, variants, ntiles, args.steps, args.warmup, dist,
                          world, rank, forward=args.forward, e2e_leg=args.e2e, align=args.align)

@@ -124,19 +124,47 @@ class TileBatch:
 
     @classmethod
     def from_packed(cls, packed: np.ndarray, in_off, in_size, out_sizes, device: int = 0,
-                    fill: int = 0) -> "TileBatch":
+                    fill: int = 0, arena=None, in_first: bool = False, gap: int = 0) -> "TileBatch":
+        """arena: an optional device uint8 tensor of at least
+        arena_bytes(packed.size, sum(out_sizes)) bytes; the outputs then sit at
+        its start and the filtered tiles at the next 2 MiB boundary after them,
+        so batches built in turn on one arena use the same device pages."""
         import torch
         dev = torch.device("cuda", device)
         packed = np.ascontiguousarray(packed, dtype=np.uint8)
-        d_in = torch.from_numpy(packed).to(dev) if packed.size else torch.zeros(16, dtype=torch.uint8,
-                                                                                device=dev)
         out_size = np.asarray(out_sizes, dtype=np.uint64)
         out_off = np.zeros_like(out_size)
         if out_size.size:
             out_off[1:] = np.cumsum(out_size)[:-1]
         total = int(out_size.sum()) if out_size.size else 0
+        if arena is not None:
+            need = cls.arena_bytes(packed.size, total)
+            if arena.numel() < need:
+                raise ValueError(f"arena of {arena.numel()} B < {need} B")
+            ob = max(total, 16)
+            if in_first:  # (layout experiments: tiles first, outputs after)
+                d_in = arena[:max(packed.size, 16)]
+                o0 = -(-max(packed.size, 16) // (2 << 20)) * (2 << 20) + gap
+                d_out = arena[o0:o0 + ob]
+            else:
+                d_out = arena[:ob]
+                ib = -(-ob // (2 << 20)) * (2 << 20) + gap
+                d_in = arena[ib:ib + max(packed.size, 16)]
+            d_out.fill_(fill)
+            if packed.size:
+                d_in[:packed.size].copy_(torch.from_numpy(packed))
+            return cls(d_in, in_off, in_size, d_out, out_off, out_size)
+        d_in = torch.from_numpy(packed).to(dev) if packed.size else torch.zeros(16, dtype=torch.uint8,
+                                                                                device=dev)
         d_out = torch.full((max(total, 16),), fill, dtype=torch.uint8, device=dev)
         return cls(d_in, in_off, in_size, d_out, out_off, out_size)
+
+    @staticmethod
+    def arena_bytes(in_bytes: int, out_bytes: int) -> int:
+        """Bytes from_packed(arena=...) needs for in_bytes of filtered tiles and
+        out_bytes of outputs."""
+        ob = max(out_bytes, 16)
+        return -(-ob // (2 << 20)) * (2 << 20) + -(-max(in_bytes, 16) // (2 << 20)) * (2 << 20)
 
     @classmethod
     def from_host(cls, tiles: Sequence, out_sizes, device: int = 0, fill: int = 0,

@@ -3,12 +3,12 @@
 # rather than on the kernel?  100,000 tiles, one box, bench.py legs in order.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/order_${1:-x}
+OUT=$R/gpurun_out/r05/order_${1:-x}
 mkdir -p $OUT
 cd $R
 run() {  # name, bench args... (later flags win: --e2e / --forward turn the legs back on)
   local n=$1; shift
-  timeout -k 10 240 python -u bench.py --no-others --no-e2e --no-forward --no-cpu-baseline --shard-tiles 0 "$@" \
+  timeout -k 10 240 python -u bench.py --no-others --no-e2e --no-forward --no-cpu-baseline --shard-tiles 0 --c5s-tiles 0 "$@" \
     > $OUT/$n.json 2> $OUT/$n.err || { echo "$n failed"; tail -20 $OUT/$n.err; exit 11; }
   python -c "
 import json; d=json.loads([l for l in open('$OUT/$n.json') if l.startswith('{')][-1]); v=d['config']['variants']
