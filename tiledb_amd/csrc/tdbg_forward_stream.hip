@@ -50,8 +50,6 @@
 namespace tdbg {
 namespace fws {
 
-constexpr int NT = 512;
-constexpr int NWV = NT / 64;
 constexpr uint32_t NV = 16384;              // int32 values per tile
 constexpr uint32_t TB = NV * 4;             // tile bytes
 constexpr uint32_t NWMAX = 257;             // BWR windows over <= 65,562 DD-output bytes
@@ -61,17 +59,28 @@ constexpr uint32_t X0 = DELTA - 2;          // compressed data byte 0
 constexpr uint32_t DOUT_MAX = 17 + 9 + TB;  // DD output bytes (raw)
 constexpr uint32_t BDW = (DELTA + DOUT_MAX + 320 + 15) / 16 * 4;  // image dwords (+ reads past the last window)
 constexpr uint32_t WD0 = (DELTA + 34) / 4;  // LDS dword of DD word 0
-constexpr uint32_t WPP = NT / 8;                          // BWR windows per pass (8 lanes each)
-constexpr uint32_t PASSES = (NWMAX + WPP - 1) / WPP;        // BWR window passes (5)
 static_assert(DELTA % 4 == 2 && X0 >= 20 + MLMAX, "LDS image layout");
+constexpr uint32_t GRID_CAP = 1u << 22;
 
+// NT threads per workgroup: 512 (persistent grid, two workgroups per CU at
+// 128 VGPRs) or 1024 (one workgroup per tile, two per CU at 64 VGPRs); a
+// thread owns UPT = 4096 / NT of the tile's 16-B units
+template <int NT>
+struct Cfg {
+  static constexpr int NWV = NT / 64;
+  static constexpr uint32_t UPT = 4096 / NT;                 // units (runs of UPT values per plane) per thread
+  static constexpr uint32_t WPP = NT / 8;                    // BWR windows per pass (8 lanes each)
+  static constexpr uint32_t PASSES = (NWMAX + WPP - 1) / WPP;  // BWR window passes
+};
+
+template <int NT>
 struct Lds {
   uint32_t B[BDW];
   uint32_t wcs[NWMAX + 7];   // window compressed bytes, then (after the scan) its data offset
   uint32_t wbits[NWMAX + 7]; // the window's bits field
   int32_t wmin[NWMAX + 7];
-  uint64_t red[4 * NWV];
-  uint32_t scan[NWV];
+  uint64_t red[4 * Cfg<NT>::NWV];
+  uint32_t scan[Cfg<NT>::NWV];
   uint64_t clk[8];  // diagnostics: phase clocks (TDBG_PROF)
 };
 
@@ -119,8 +128,10 @@ __device__ __forceinline__ void tr4(uint32_t p0, uint32_t p1, uint32_t p2, uint3
   w[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
 }
 
-__device__ __forceinline__ void lds_byte(Lds& L, uint32_t o, uint32_t v) { ((uint8_t*)L.B)[o] = (uint8_t)v; }
-__device__ __forceinline__ void lds_u32b(Lds& L, uint32_t o, uint32_t v) {
+template <class LDS>
+__device__ __forceinline__ void lds_byte(LDS& L, uint32_t o, uint32_t v) { ((uint8_t*)L.B)[o] = (uint8_t)v; }
+template <class LDS>
+__device__ __forceinline__ void lds_u32b(LDS& L, uint32_t o, uint32_t v) {
 #pragma unroll
   for (int i = 0; i < 4; i++) lds_byte(L, o + i, v >> (8 * i));
 }
@@ -170,17 +181,18 @@ __device__ __forceinline__ uint64_t row_max64(uint64_t v) {
 // region was zeroed before B1).  Thread 0's plane-0 run has codes from
 // position 2 only: it is packed with two zero codes in front at stream bit
 // -2 CB and its chunks below 0 are not written.
-template <int CB>
-__device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint32_t T) {
+template <int CB, int NT>
+__device__ __forceinline__ void dd_emit(Lds<NT>& L, const uint32_t (&S)[Cfg<NT>::UPT + 2][4], uint32_t T) {
+  constexpr int UPT = (int)Cfg<NT>::UPT;
   constexpr uint32_t BS = CB - 1;            // bitsize
-  constexpr int JF = (8 * CB) / 32 - 1;      // chunks 1..JF lie inside the run for any start bit
-  constexpr int JX = (8 * CB + 30) / 32;     // the last chunk a run can reach
+  constexpr int JF = (UPT * CB) / 32 - 1;    // chunks 1..JF lie inside the run for any start bit
+  constexpr int JX = (UPT * CB + 30) / 32;   // the last chunk a run can reach
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    uint32_t code[8];
+    uint32_t code[UPT];
     uint32_t dprev = S[1][k] - S[0][k];
 #pragma unroll
-    for (int i = 2; i < 10; i++) {
+    for (int i = 2; i < UPT + 2; i++) {
       // (coded: |dd| < 2^30, so the wrapped 32-bit value is exact)
       const uint32_t d = S[i][k] - S[i - 1][k];
       const int32_t dd = (int32_t)(d - dprev);
@@ -193,11 +205,11 @@ __device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint
       code[0] = t0 ? 0u : code[0];
       code[1] = t0 ? 0u : code[1];
     }
-    uint32_t R[8];
+    uint32_t R[UPT];
 #pragma unroll
-    for (int j = 0; j < 8; j++) R[j] = 0;
+    for (int j = 0; j < UPT; j++) R[j] = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < UPT; j++) {
       const int off = j * CB, w0 = off >> 5, sh = off & 31;
       if (sh + CB <= 32) {
         R[w0] |= code[j] << (32 - sh - CB);
@@ -206,8 +218,8 @@ __device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint
         R[w0 + 1] |= code[j] << (64 - sh - CB);
       }
     }
-    // stream bit of the run's first code (code index 4096 k + 8 T - 2)
-    const int32_t B0 = ((int32_t)(4096 * k) + 8 * (int32_t)T - 2) * CB;
+    // stream bit of the run's first code (code index 4096 k + UPT T - 2)
+    const int32_t B0 = ((int32_t)(4096 * k) + UPT * (int32_t)T - 2) * CB;
     const int32_t c0 = B0 >> 5;
     const uint32_t nb0 = (uint32_t)B0 & 31u;
     const int32_t base = (int32_t)WD0 + (c0 & ~1);
@@ -216,10 +228,10 @@ __device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint
     // (odd j) base - 1 + 3 par + j
     uint32_t* const pe = L.B + (base + 1 - (int32_t)par);
     uint32_t* const po = L.B + (base - 1 + 3 * (int32_t)par);
-    const int32_t jmax = (int32_t)((8 * CB - 1 + nb0) >> 5);
+    const int32_t jmax = (int32_t)((UPT * CB - 1 + nb0) >> 5);
 #pragma unroll
     for (int j = 0; j <= JX; j++) {
-      const uint32_t hi = j == 0 ? 0u : R[j - 1], lo = j == 8 ? 0u : R[j];
+      const uint32_t hi = j == 0 ? 0u : R[j - 1], lo = j >= UPT ? 0u : R[j];
       const uint32_t ch = __builtin_amdgcn_alignbit(hi, lo, nb0);
       uint32_t* const dst = (j & 1 ? po : pe) + j;
       const bool inside = k != 0 || c0 + j >= 0;  // (thread 0, plane 0: no chunks below 0)
@@ -232,25 +244,43 @@ __device__ __forceinline__ void dd_emit(Lds& L, const uint32_t (&S)[10][4], uint
   }
 }
 
-template <bool SGN>
-__global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams kp) {
-  __shared__ Lds L;
+// The tile loop: NT = 512 walks tiles blockIdx.x, + gridDim.x, ... (the next
+// tile's units loaded behind this one's stores); NT = 1024 takes the one work
+// item (b & 7) * ceil(cnt / 8) + (b >> 3) of [base, base + cnt): each XCD
+// (workgroups are dealt round-robin over the 8) works through a contiguous
+// eighth of the launch (placement assumption for speed only).
+template <bool SGN, int NT>
+__device__ __forceinline__ void filter_c5_body(const KParams& kp, uint32_t base, uint32_t cnt) {
+  constexpr bool PERSIST = NT == 512;
+  constexpr int NWV = Cfg<NT>::NWV;
+  constexpr uint32_t UPT = Cfg<NT>::UPT, WPP = Cfg<NT>::WPP, PASSES = Cfg<NT>::PASSES;
+  __shared__ Lds<NT> L;
   Clock pc;
-  pc.init(kp.prof, L.clk);
+  // (phase clocks of the first 512 workgroups: the profile buffer's rows)
+  pc.init(PERSIST || blockIdx.x < 512 ? kp.prof : nullptr, L.clk);
   auto shape_of = [&](uint64_t jj) {
     const uint8_t* ii = kp.in[jj];
     return kp.in_size[jj] == TB && (((uintptr_t)ii) & 15) == 0 && (((uintptr_t)kp.out[jj]) & 15) == 0 &&
            kp.out_size[jj] >= 64;
   };
-  v4u U[10];
+  v4u U[UPT + 2];
   auto load_units = [&](uint64_t jj, uint32_t T) {
-    // units 8T..8T+7 and the two before (wrapping into the last plane's end for T = 0)
+    // units UPT T..UPT T + UPT - 1 and the two before (wrapping into the last
+    // plane's end for T = 0)
     const g_cu4* src = (const g_cu4*)kp.in[jj];
 #pragma unroll
-    for (int i = 0; i < 10; i++) U[i] = src[(8 * T + i - 2) & 4095u];
+    for (uint32_t i = 0; i < UPT + 2; i++) U[i] = src[(UPT * T + i - 2) & 4095u];
   };
   bool pre = false;  // U holds this tile's units already (loaded at the end of the last iteration)
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
+  uint64_t j0 = blockIdx.x, jstep = gridDim.x;
+  if (!PERSIST) {
+    const uint32_t n8 = (cnt + 7) >> 3;
+    const uint32_t jj = (blockIdx.x & 7) * n8 + (blockIdx.x >> 3);
+    if (jj >= cnt) return;
+    j0 = (uint64_t)base + jj;
+    jstep = ~0ull >> 1;  // (one tile)
+  }
+  for (uint64_t j = j0; j < kp.ntiles; j += jstep) {
     // thread index opaque to the optimizer: the unrolled per-thread index
     // math is tile-invariant, and hoisting it out of the tile loop pins (and
     // spills) dozens of registers
@@ -273,10 +303,10 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       // ---- zero the DD word region (codes are OR-ed in) ----
       static_assert(BDW % 4 == 0, "16-B zeroing");
       for (uint32_t d = (WD0 & ~3u) + 4 * T; d < BDW; d += 4 * NT) *(v4u*)(L.B + d) = v4u{0u, 0u, 0u, 0u};
-      // S[i][k]: position 8T + i - 2 of plane k (for T = 0 and i < 2: plane k-1's end)
-      uint32_t S[10][4];
+      // S[i][k]: position UPT T + i - 2 of plane k (for T = 0 and i < 2: plane k-1's end)
+      uint32_t S[UPT + 2][4];
 #pragma unroll
-      for (int i = 0; i < 10; i++) tr4(U[i].x, U[i].y, U[i].z, U[i].w, S[i]);
+      for (uint32_t i = 0; i < UPT + 2; i++) tr4(U[i].x, U[i].y, U[i].z, U[i].w, S[i]);
       if (T == 0) {
 #pragma unroll
         for (int i = 0; i < 2; i++) {
@@ -298,8 +328,8 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         auto f = [&](uint32_t v) { return SGN ? (double)(int32_t)v : (double)v; };
         double x2 = f(S[0][k]), x1 = f(S[1][k]);
 #pragma unroll
-        for (int i = 2; i < 10; i++) {
-          const uint32_t P = 4096 * k + 8 * T + i - 2;
+        for (uint32_t i = 2; i < UPT + 2; i++) {
+          const uint32_t P = 4096 * k + UPT * T + i - 2;
           const double x = f(S[i][k]);
           const double d = x - x1, dp = x1 - x2;
           double a = __builtin_fabs(d - dp);
@@ -333,7 +363,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       // (the 64-bit extensions of the bit-size pass are recomputed below, not
       // kept live across the barrier: 40 values would take 80 registers)
 #pragma unroll
-      for (int i = 0; i < 10; i++)
+      for (uint32_t i = 0; i < UPT + 2; i++)
 #pragma unroll
         for (int k = 0; k < 4; k++) asm volatile("" : "+v"(S[i][k]));
       const uint32_t bitsize = mx ? 64 - __builtin_clzll(mx) : 1;  // do { ++b; m >>= 1; } while (m)
@@ -361,7 +391,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
 #pragma unroll
         for (int k = 0; k < 4; k++)
 #pragma unroll
-          for (int i = 2; i < 10; i++) L.B[(DELTA + 26) / 4 + 4096 * k + 8 * T + i - 2] = S[i][k];
+          for (uint32_t i = 2; i < UPT + 2; i++) L.B[(DELTA + 26) / 4 + 4096 * k + UPT * T + i - 2] = S[i][k];
       } else {
         if (T == 0) {
           L.B[(DELTA + 26) / 4] = S[2][0];
@@ -370,7 +400,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
         // one instantiation per code width (uniform)
         switch (__builtin_amdgcn_readfirstlane(cb)) {
 #define TDBG_FCB(c) \
-  case c: dd_emit<c>(L, S, T); break;
+  case c: dd_emit<c, NT>(L, S, T); break;
           TDBG_FCB(2) TDBG_FCB(3) TDBG_FCB(4) TDBG_FCB(5) TDBG_FCB(6) TDBG_FCB(7) TDBG_FCB(8) TDBG_FCB(9)
           TDBG_FCB(10) TDBG_FCB(11) TDBG_FCB(12) TDBG_FCB(13) TDBG_FCB(14) TDBG_FCB(15) TDBG_FCB(16)
           TDBG_FCB(17) TDBG_FCB(18) TDBG_FCB(19) TDBG_FCB(20) TDBG_FCB(21) TDBG_FCB(22) TDBG_FCB(23)
@@ -387,26 +417,34 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       // into registers ----
       const uint32_t nw = (Ld + 255) / 256;
       const uint32_t g = T >> 3, li = T & 7;
-      uint32_t E[PASSES][8];
+      // (NT = 1024: the elements are read again for the compression, one pass
+      // at a time, instead of held in registers across B3-B5 -- 64 VGPRs)
+      constexpr bool REREAD = !PERSIST;
+      constexpr uint32_t EP = REREAD ? 1 : PASSES;
+      uint32_t E[EP][8];
+      // DD-output bytes [256 wi + 32 li, +32) = LDS dwords from 592 + 64 wi + 8 li, shifted by 2
+      // (windows 2, 3 mod 4 read their second half first: every
+      // ds_read_b128 lane group then covers 64 distinct banks)
+      auto load_win = [&](uint32_t wi, uint32_t (&e8)[8]) {
+        const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 8 * li;
+        const uint32_t hs = 4 * ((wi >> 1) & 1);
+        const v4u qa = *(const v4u*)(L.B + d0 + hs), qb = *(const v4u*)(L.B + d0 + 4 - hs);
+        const uint32_t q8 = L.B[d0 + 8];
+        const bool sw = hs != 0;
+        const v4u q0 = sw ? qb : qa, q1 = sw ? qa : qb;
+        const uint32_t Q[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
+#pragma unroll
+        for (int e = 0; e < 8; e++) e8[e] = __builtin_amdgcn_alignbyte(Q[e + 1], Q[e], 2);
+      };
 #pragma unroll
       for (uint32_t p = 0; p < PASSES; p++) {
         const uint32_t wi = WPP * p + g;
+        const uint32_t ep = REREAD ? 0 : p;
 #pragma unroll
-        for (int e = 0; e < 8; e++) E[p][e] = 0;
+        for (int e = 0; e < 8; e++) E[ep][e] = 0;
         if (WPP * p < nw) {  // (uniform)
           if (wi < nw) {  // (uniform over the window's 8 lanes)
-            // DD-output bytes [256 wi + 32 li, +32) = LDS dwords from 592 + 64 wi + 8 li, shifted by 2
-            // (windows 2, 3 mod 4 read their second half first: every
-            // ds_read_b128 lane group then covers 64 distinct banks)
-            const uint32_t d0 = (DELTA - 2) / 4 + 64 * wi + 8 * li;
-            const uint32_t hs = 4 * ((wi >> 1) & 1);
-            const v4u qa = *(const v4u*)(L.B + d0 + hs), qb = *(const v4u*)(L.B + d0 + 4 - hs);
-            const uint32_t q8 = L.B[d0 + 8];
-            const bool sw = hs != 0;
-            const v4u q0 = sw ? qb : qa, q1 = sw ? qa : qb;
-            const uint32_t Q[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
-#pragma unroll
-            for (int e = 0; e < 8; e++) E[p][e] = __builtin_amdgcn_alignbyte(Q[e + 1], Q[e], 2);
+            load_win(wi, E[ep]);
             const uint32_t nb = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
             const uint32_t ne = nb >> 2;
             auto mm = [&](uint32_t v, uint32_t& mn, uint32_t& mx) {
@@ -418,16 +456,16 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
                 mx = v > mx ? v : mx;
               }
             };
-            uint32_t mn32 = E[p][0], mx32 = E[p][0];
+            uint32_t mn32 = E[ep][0], mx32 = E[ep][0];
             if (ne == 64) {  // every window but the last: all 8 elements count
 #pragma unroll
-              for (int e = 1; e < 8; e++) mm(E[p][e], mn32, mx32);
+              for (int e = 1; e < 8; e++) mm(E[ep][e], mn32, mx32);
             } else {
               mn32 = SGN ? 0x7fffffffu : 0xffffffffu;
               mx32 = SGN ? 0x80000000u : 0u;
 #pragma unroll
               for (int e = 0; e < 8; e++)
-                if (8 * li + e < ne) mm(E[p][e], mn32, mx32);
+                if (8 * li + e < ne) mm(E[ep][e], mn32, mx32);
             }
             half_minmax<SGN>(mn32, mx32);
             if (li == 0) {
@@ -502,9 +540,19 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
       __syncthreads();  // B5: offsets; every element is in registers
       pc.mark(4);
       // ---- compressed windows, in place below the DD output ----
+      // (REREAD: pass p reads its windows' elements, a barrier, then writes:
+      // a window's output [off, off + cs) lies below 256 (wi + 1), so a pass's
+      // writes never reach a later pass's inputs, and inside a pass every read
+      // is done before any write)
 #pragma unroll
       for (uint32_t p = 0; p < PASSES; p++) {
         const uint32_t wi = WPP * p + g;
+        const uint32_t ep = REREAD ? 0 : p;
+        if (REREAD) {
+          if (WPP * p >= nw) break;  // (uniform)
+          if (wi < nw) load_win(wi, E[ep]);
+          __syncthreads();
+        }
         if (WPP * p < nw && wi < nw) {
           const uint32_t off = L.wcs[wi], bits = L.wbits[wi];
           const uint32_t nbw = Ld - 256 * wi < 256 ? Ld - 256 * wi : 256;
@@ -513,7 +561,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
           const uint32_t a = X0 + off;  // 4-aligned: every earlier window's size is a multiple of 4
           uint32_t r[8];
 #pragma unroll
-          for (int e = 0; e < 8; e++) r[e] = E[p][e] - mnv;
+          for (int e = 0; e < 8; e++) r[e] = E[ep][e] - mnv;
           if (kind == 0) {
             uint32_t x0 = 0, x1 = 0;
 #pragma unroll
@@ -527,8 +575,8 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
                 v4u{(r[0] & 0xffffu) | (r[1] << 16), (r[2] & 0xffffu) | (r[3] << 16), (r[4] & 0xffffu) | (r[5] << 16),
                     (r[6] & 0xffffu) | (r[7] << 16)};
           } else {
-            *(v4u*)(L.B + (a >> 2) + 8 * li) = v4u{E[p][0], E[p][1], E[p][2], E[p][3]};
-            *(v4u*)(L.B + (a >> 2) + 8 * li + 4) = v4u{E[p][4], E[p][5], E[p][6], E[p][7]};
+            *(v4u*)(L.B + (a >> 2) + 8 * li) = v4u{E[ep][0], E[ep][1], E[ep][2], E[ep][3]};
+            *(v4u*)(L.B + (a >> 2) + 8 * li + 4) = v4u{E[ep][4], E[ep][5], E[ep][6], E[ep][7]};
           }
         }
       }
@@ -570,7 +618,7 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
     }
     // the next tile's units, behind this tile's stores
     pre = false;
-    if (j + gridDim.x < kp.ntiles && shape_of(j + gridDim.x)) {
+    if (PERSIST && j + gridDim.x < kp.ntiles && shape_of(j + gridDim.x)) {
       uint32_t Tn = threadIdx.x;
       asm volatile("" : "+v"(Tn));
       load_units(j + gridDim.x, Tn);
@@ -587,13 +635,37 @@ __global__ void __launch_bounds__(NT, 4) filter_stream_c5_kernel(const KParams k
   pc.flush();
 }
 
+template <bool SGN>
+__global__ void __launch_bounds__(512, 4) filter_stream_c5_kernel(const KParams kp) {
+  filter_c5_body<SGN, 512>(kp, 0, 0);
+}
+
+template <bool SGN>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+filter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
+  filter_c5_body<SGN, 1024>(kp, base, cnt);
+}
+
 }  // namespace fws
 }  // namespace tdbg
 
 // sgn: the DD and BWR stages' integer type (INT32 / UINT32) is signed
-extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s) {
+// tile: one 1024-thread workgroup per tile (grid = the tiles, launches of at
+// most GRID_CAP), else the persistent 512-thread kernel on `grid` workgroups
+extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, int tile, hipStream_t s) {
   using namespace tdbg::fws;
-  if (sgn) hipLaunchKernelGGL((filter_stream_c5_kernel<true>), dim3(grid), dim3(NT), 0, s, *kp);
-  else hipLaunchKernelGGL((filter_stream_c5_kernel<false>), dim3(grid), dim3(NT), 0, s, *kp);
-  return hipGetLastError();
+  if (!tile) {
+    if (sgn) hipLaunchKernelGGL((filter_stream_c5_kernel<true>), dim3(grid), dim3(512), 0, s, *kp);
+    else hipLaunchKernelGGL((filter_stream_c5_kernel<false>), dim3(grid), dim3(512), 0, s, *kp);
+    return hipGetLastError();
+  }
+  for (uint64_t b = 0; b < kp->ntiles; b += GRID_CAP) {
+    const uint32_t cnt = (uint32_t)(kp->ntiles - b < GRID_CAP ? kp->ntiles - b : GRID_CAP);
+    const uint32_t g = 8 * ((cnt + 7) / 8);
+    if (sgn) hipLaunchKernelGGL((filter_c5tile_kernel<true>), dim3(g), dim3(1024), 0, s, *kp, (uint32_t)b, cnt);
+    else hipLaunchKernelGGL((filter_c5tile_kernel<false>), dim3(g), dim3(1024), 0, s, *kp, (uint32_t)b, cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }

@@ -34,7 +34,8 @@ extern "C" hipError_t tdbg_launch_general(const tdbg::KParams* kp, uint32_t grid
 extern "C" hipError_t tdbg_launch_fixup(const tdbg::KParams* kp, uint32_t grid,
                                         hipStream_t stream);
 extern "C" hipError_t tdbg_launch_filter(const tdbg::KParams* kp, uint32_t grid, hipStream_t stream);
-extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
+extern "C" hipError_t tdbg_launch_filter_c5(const tdbg::KParams* kp, uint32_t grid, int sgn, int tile,
+                                           hipStream_t s);
 extern "C" hipError_t tdbg_launch_filter_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                hipStream_t s);
 extern "C" hipError_t tdbg_launch_filter_shuffle4(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
@@ -644,6 +645,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   uint32_t grid;
   if (fast) {
     grid = tdbg_fast_grid(p->plan.fast, c->cus);
+    static const long fg = tdbg_hook_int("TDBG_FAST_GRID", 0);  // experiments: e.g. one tile per workgroup
+    if (fg > 0) grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), (uint64_t)fg);
   } else {
     grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)c->cus * 8);
   }
@@ -1169,7 +1172,10 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kf.fbq_cap = (uint32_t)n;
     kf.stats = c->d_stats;
     static const bool prof = tdbg_hook("TDBG_PROF") != nullptr;  // diagnostics: phase clocks
-    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
+    // one 1024-thread workgroup per tile (tdbg_forward_stream.hip); the
+    // persistent 512-thread grid stays as the A/B reference (experiments)
+    static const bool persist = tdbg_hook("TDBG_FWD_PERSIST") != nullptr;
+    const uint32_t fgrid = persist ? (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2) : 512u;
     if (prof) {
       if (c->prof_grid < fgrid) {
         if (c->d_prof) (void)hipFree(c->d_prof);
@@ -1181,7 +1187,7 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
       HIP_OK(hipMemsetAsync(c->d_prof, 0, sizeof(uint64_t) * TDBG_PROF_PHASES * c->prof_grid, s));
       kf.prof = c->d_prof;
     }
-    e = tdbg_launch_filter_c5(&kf, fgrid, P.s[2].sgn ? 1 : 0, s);
+    e = tdbg_launch_filter_c5(&kf, fgrid, P.s[2].sgn ? 1 : 0, persist ? 0 : 1, s);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward stream launch: ") + hipGetErrorString(e));
     kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
     kp.ntiles_dev = c->d_fbq;
