@@ -688,6 +688,86 @@ def headline_line(args, W, variants, res, world):
     return line
 
 
+def dense_var_leg(engine, ctx, steps: int, tiles_side: int = 32, seed: int = 9, pinned: bool = False):
+    """The step after the path for a var-sized attribute (SURVEY 8(f) 4,
+    dense_reader.cc:1555-2007): tdbg_dense_read_var_host from host FILTERED
+    offsets tiles ([POSITIVE_DELTA(1024), BWR(256)] on uint64) and var tiles
+    ([BITSHUFFLE] on uint8) -> H2D -> unfilter (offsets with the extra offset)
+    -> cell sizes -> device scan -> byte gather -> D2H of the result offsets
+    and bytes.  One fragment over a tiles_side^2 grid of 64 x 128-cell space
+    tiles (8,192 cells of U{0..32} bytes each), subarray = the array, row
+    major; 16 unique tile pairs (encoded on the device by tdbg_filter_tiles),
+    replicated into one host block.  Rate = result bytes (offsets + var
+    bytes) / wall time per call; host buffers are pageable, as a reader's
+    would be."""
+    from tiledb_amd.filter_pipeline import (BitshuffleFilter, BitWidthReductionFilter, Datatype,
+                                            FilterPipeline, PositiveDeltaFilter)
+    rng = np.random.default_rng(seed)
+    ext = (64, 128)
+    nct = ext[0] * ext[1]
+    offp = FilterPipeline(65536, [PositiveDeltaFilter(1024), BitWidthReductionFilter(256)]).serialize()
+    varp = FilterPipeline(65536, [BitshuffleFilter()]).serialize()
+    dpo = engine.DevicePipeline(offp, 23, int(Datatype.UINT64), 8)
+    dpv = engine.DevicePipeline(varp, 23, int(Datatype.UINT8), 1)
+    offs_w, vars_ = [], []
+    for _ in range(16):
+        lens = rng.integers(0, 33, nct)
+        o = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        offs_w.append(o[:-1].copy())
+        vars_.append(rng.integers(0, 256, int(o[-1]), dtype=np.uint8))
+    st1, fo = ctx.filter(dpo, [x.view(np.uint8) for x in offs_w])
+    st2, fv = ctx.filter(dpv, vars_)
+    if st1.any() or st2.any():
+        raise SystemExit("dense var leg: device encode failed")
+    nt = tiles_side * tiles_side
+    starts = np.array([(r * ext[0], c * ext[1]) for r in range(tiles_side) for c in range(tiles_side)], dtype=np.int64)
+    hi = (tiles_side * ext[0] - 1, tiles_side * ext[1] - 1)
+    idx = [t % 16 for t in range(nt)]
+    # the filtered tiles back to back in one host block, [offsets tile, var
+    # tile] per space tile, as a FilteredData block holds a batch's reads
+    import torch
+    sz = [(len(fo[i]), len(fv[i])) for i in idx]
+    hbytes = lambda nb: (torch.empty(nb, dtype=torch.uint8, pin_memory=True).numpy() if pinned  # noqa: E731
+                         else np.empty(nb, dtype=np.uint8))
+    blk = hbytes(sum(a + b for a, b in sz))
+    off_f, var_f, o = [], [], 0
+    for i, (a, b) in zip(idx, sz):
+        blk[o:o + a] = fo[i]
+        off_f.append(blk[o:o + a])
+        blk[o + a:o + a + b] = fv[i]
+        var_f.append(blk[o + a:o + a + b])
+        o += a + b
+    var_u = [vars_[i].size for i in idx]
+    fc = engine.dense_frag_config(8, ext, (0, 0), hi, 1, 1, 0, 0)
+    dom = np.array([[0, hi[0], 0, hi[1]]], dtype=np.int64)
+    cap = sum(var_u) + 64
+    ro_buf = hbytes(nt * nct * 8).view(np.uint64)
+    rv_buf = hbytes(cap)
+    call = lambda: engine.dense_read_var_host(ctx, dpo, dpv, fc, starts, dom, off_f, var_f, var_u, b"\0", cap,  # noqa: E731
+                                              out_offsets=ro_buf, out_var=rv_buf)
+    rc, ro, rv, st = call()
+    rv = bytes(rv)
+    if rc or st.any() or len(rv) != sum(var_u):
+        raise SystemExit(f"dense var leg failed: rc {rc}")
+    # (the result's first cell row -- row 0 of every tile of the first tile
+    # row -- must be those cells' source bytes)
+    row0 = b"".join(vars_[idx[c]][: int(offs_w[idx[c]][ext[1]])].tobytes() for c in range(tiles_side))
+    if not rv.startswith(row0) or int(ro[1]) != int(offs_w[idx[0]][1]):
+        raise SystemExit("dense var leg: result bytes differ from the source cells")
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    el = (time.perf_counter() - t0) / steps
+    res_bytes = nt * nct * 8 + len(rv)
+    return {"workload": f"dense var-sized attribute, 1 fragment, {nt} space tiles of 64 x 128 cells "
+                        f"(U{{0..32}} B each), offsets [PD(1024), BWR(256)] uint64 + var [BITSHUFFLE] uint8, "
+                        "host filtered tiles -> result offsets + bytes on the host",
+            "entry": "tdbg_dense_read_var_host", "steps": steps,
+            "host_buffers": "pinned" if pinned else "pageable",
+            "result_bytes": res_bytes, "filtered_bytes": int(sum(len(x) for x in off_f) + sum(len(x) for x in var_f)),
+            "ms_per_call": round(el * 1e3, 3), "GiBps_result": round(res_bytes / el / 2**30, 2)}
+
+
 def init_dist(dist_mod, torch, env, local: int) -> str:
     """One process per GPU: RCCL ('nccl') bound to the rank's own device
     (init_process_group(device_id=cuda:local)), or the gloo rehearsal
@@ -821,6 +901,9 @@ def main():
                 "tiles": args.shard_tiles, "steps": args.steps, "variants": sh,
                 "min_over_variants_GiBps": round(min(x["GiBps"] for x in sh.values()), 2),
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sh.values()), 4)}
+        line["config"]["dense_read_var_host"] = {
+            "pageable": dense_var_leg(engine, ctx, max(2, args.steps // 4)),
+            "pinned": dense_var_leg(engine, ctx, max(2, args.steps // 4), pinned=True)}
         # the C5 pipeline on 40,000-B tiles (one chunk of 10,000 values: not
         # 64 KiB, byte planes not 16-B aligned), the same output bytes
         if args.c5s_tiles:

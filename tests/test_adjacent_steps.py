@@ -384,7 +384,14 @@ _FRAGS = [((3, 4), (8, 16), (2, 3), (21, 60), 3, 0, 0, False),
           ((3, 4), (8, 16), (0, 0), (23, 63), 2, 1, 0, True),
           ((3, 4), (8, 16), (5, 9), (20, 50), 4, 0, 1, True),
           ((2, 2, 3), (4, 8, 8), (1, 0, 3), (7, 14, 20), 3, 1, 1, False),
-          ((5,), (512,), (100,), (2400,), 0, 0, 0, True)]
+          ((5,), (512,), (100,), (2400,), 0, 0, 0, True),
+         # one fragment: slab copies where its domain holds a tile's whole
+         # region in the result's order, cell copies elsewhere
+         ((3, 4), (8, 16), (2, 3), (21, 60), 1, 0, 0, True),
+         ((3, 4), (8, 16), (0, 0), (23, 63), 1, 1, 1, False),
+         ((3, 4), (8, 16), (1, 2), (22, 61), 1, 0, 1, True),
+         ((2, 2, 3), (4, 8, 8), (1, 0, 3), (7, 14, 20), 1, 1, 1, True),
+         ((5,), (512,), (100,), (2400,), 1, 0, 0, False)]
 
 
 @pytest.mark.gpu
@@ -393,11 +400,33 @@ def test_dense_copy_fragments(oracle_mod, case):
     """copy_fixed_tiles with several overlapping fragments, absent tiles, the
     fill value and validity (nullable), on device tiles: bit-exact against
     the oracle's restatement (dense_reader.cc:1555-1750)."""
+    _check_fragments(oracle_mod, case)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [c for c in _FRAGS if c[4] == 1], ids=lambda c: f"t{'x'.join(map(str, c[0]))}_o{c[5]}l{c[6]}")
+@pytest.mark.parametrize("cover", ["whole", "most"])
+def test_dense_copy_one_fragment_slabs(oracle_mod, case, cover):
+    """One fragment whose domain holds the whole array (every tile's region
+    goes through the slab copier when the orders agree) or all of it but the
+    last cell row / column of every dimension (the edge tiles fall back to
+    cell copies, the fill value beyond the domain): bit-exact."""
+    shape_tiles, ext = case[0], case[1]
+    full = [t * e for t, e in zip(shape_tiles, ext)]
+    hi = [f - 1 - (1 if cover == "most" else 0) for f in full]
+    _check_fragments(oracle_mod, case, doms=[[(0, h) for h in hi]])
+
+
+def _check_fragments(oracle_mod, case, doms=None):
     import torch
     from tiledb_amd import engine
     shape_tiles, ext, lo, hi, nfrag, cell_order, layout, nullable = case
     rng = np.random.default_rng(nfrag * 7 + cell_order + 3 * layout + len(ext))
-    doms, starts, present = _frag_layout(rng, shape_tiles, ext, nfrag)
+    rdoms, starts, present = _frag_layout(rng, shape_tiles, ext, nfrag)
+    if doms is not None:  # (every tile present)
+        present = [[True] * nfrag for _ in present]
+    else:
+        doms = rdoms
     ncell_t = int(np.prod(ext))
     cs = 8
     tiles = [[rng.integers(0, 256, ncell_t * cs, dtype=np.uint8) if present[t][f] else None

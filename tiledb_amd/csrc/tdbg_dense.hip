@@ -229,6 +229,64 @@ __device__ __forceinline__ uint8_t valid_at(const uint8_t* const* validity, uint
   return v ? v[pos] : (uint8_t)1;
 }
 
+// The region R of a tile copied slab by slab (the tile's cell order equals
+// the result layout): each run along the fastest dimension is contiguous on
+// both sides, moved by the whole workgroup in 16/4/1-byte vectors
+// (dense_reader.cc:1555-1748, a memcpy per cell slab).  cs = 1 with a NULL
+// src writes `one` bytes (the validity of a fragment given without one).
+__device__ void copy_region_slabs(const tdbg_dense_copy_config& cfg, const Region& R, const uint8_t* src,
+                                  uint64_t cs, uint8_t* result, uint8_t one = 1) {
+  const uint32_t nd = cfg.dim_num;
+  const bool row = cfg.cell_order == 0;
+  int64_t sub_ext[TDBG_DENSE_MAX_DIMS];
+  for (uint32_t d = 0; d < nd; d++) sub_ext[d] = cfg.sub_hi[d] - cfg.sub_lo[d] + 1;
+  const uint32_t f = row ? nd - 1 : 0;
+  const uint64_t slab = (uint64_t)R.len[f] * cs;
+  const uint64_t nslab = R.ncell / (uint64_t)R.len[f];
+  for (uint64_t k = 0; k < nslab; k++) {
+    int64_t c[TDBG_DENSE_MAX_DIMS];
+    uint64_t r = k;
+    if (row) {
+      for (int d = (int)nd - 2; d >= 0; d--) {
+        c[d] = (int64_t)(r % (uint64_t)R.len[d]);
+        r /= (uint64_t)R.len[d];
+      }
+      c[nd - 1] = 0;
+    } else {
+      for (uint32_t d = 1; d < nd; d++) {
+        c[d] = (int64_t)(r % (uint64_t)R.len[d]);
+        r /= (uint64_t)R.len[d];
+      }
+      c[0] = 0;
+    }
+    int64_t ct[TDBG_DENSE_MAX_DIMS], cr[TDBG_DENSE_MAX_DIMS];
+    for (uint32_t d = 0; d < nd; d++) {
+      ct[d] = R.toff[d] + c[d];
+      cr[d] = R.lo[d] - cfg.sub_lo[d] + c[d];
+    }
+    uint8_t* d8 = result + lin(cr, sub_ext, nd, row) * cs;
+    if (!src) {
+      for (uint64_t i = threadIdx.x; i < slab; i += NT) d8[i] = one;
+      continue;
+    }
+    const uint8_t* s8 = src + lin(ct, cfg.tile_extent, nd, row) * cs;
+    if (((((uintptr_t)s8) | ((uintptr_t)d8) | slab) & 15) == 0) {
+      for (uint64_t i = threadIdx.x; i < slab / 16; i += NT) ((uint4*)d8)[i] = ((const uint4*)s8)[i];
+    } else if (((((uintptr_t)s8) | ((uintptr_t)d8) | slab) & 3) == 0) {
+      for (uint64_t i = threadIdx.x; i < slab / 4; i += NT) ((uint32_t*)d8)[i] = ((const uint32_t*)s8)[i];
+    } else {
+      for (uint64_t i = threadIdx.x; i < slab; i += NT) d8[i] = s8[i];
+    }
+  }
+}
+
+// the fragment's domain holds every cell of R
+__device__ __forceinline__ bool dom_covers(const int64_t* dom, const Region& R, uint32_t nd) {
+  bool in = true;
+  for (uint32_t d = 0; d < nd; d++) in = in && dom[2 * d] <= R.lo[d] && dom[2 * d + 1] >= R.lo[d] + R.len[d] - 1;
+  return in;
+}
+
 __global__ void __launch_bounds__(NT) dense_frag_copy_kernel(const tdbg_dense_frag_config fc, uint64_t ntiles,
                                                              const int64_t* tile_start, const int64_t* frag_dom,
                                                              const uint8_t* const* tiles,
@@ -240,6 +298,14 @@ __global__ void __launch_bounds__(NT) dense_frag_copy_kernel(const tdbg_dense_fr
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     Region R;
     if (!region_of(cfg, tile_start + t * cfg.dim_num, R)) continue;
+    // one fragment whose tile exists and whose domain holds the whole region,
+    // in the result's order: slab copies (the common single-fragment read)
+    if (fc.nfrag == 1 && tiles[t] && cfg.cell_order == cfg.layout && dom_covers(frag_dom, R, cfg.dim_num)) {
+      copy_region_slabs(cfg, R, tiles[t], cs, result);
+      if (fc.nullable && result_validity)
+        copy_region_slabs(cfg, R, validity ? validity[t] : nullptr, 1, result_validity, 1);
+      continue;
+    }
     for (uint64_t k = threadIdx.x; k < R.ncell; k += NT) {
       uint64_t pos, rc;
       const int f = cell_at(cfg, R, k, (uint32_t)t, fc.nfrag, frag_dom, tiles, pos, rc);

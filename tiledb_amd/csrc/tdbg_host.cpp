@@ -192,6 +192,8 @@ struct tdbg_context {
   uint64_t dense_src_cap = 0, dense_ncells = 0;
   uint64_t* dense_bsum = nullptr;
   uint32_t* dense_err = nullptr;  // set by the var sizes kernel: offsets outside their var tile
+  uint8_t* dv_arena = nullptr;    // tdbg_dense_read_var_host's device buffers (grow-only)
+  uint64_t dv_cap = 0;
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -600,6 +602,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->dense_src) (void)hipFree(c->dense_src);
   if (c->dense_bsum) (void)hipFree(c->dense_bsum);
   if (c->dense_err) (void)hipFree(c->dense_err);
+  if (c->dv_arena) (void)hipFree(c->dv_arena);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -2189,30 +2192,41 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
     }
   const uint64_t m = idx.size();
   const uint64_t n = dense_cells(&cfg->base);
-  std::vector<void*> bufs;
-  auto dalloc = [&](void** out, uint64_t bytes) -> bool {
-    void* q = nullptr;
-    if (hipMalloc(&q, std::max<uint64_t>(bytes, 16)) != hipSuccess) return false;
-    bufs.push_back(q);
-    *out = q;
-    return true;
+  // every device buffer of the read carved from one grow-only context arena
+  // (a hipMalloc / hipFree pair per buffer and call cost more than the read's
+  // own kernels).  The var result holds at most every present tile's var
+  // bytes plus the fill value once per cell (each result cell is one source
+  // cell or the fill), and never more than the caller's var_cap.
+  const uint64_t rvar_max = std::min<uint64_t>(var_cap, unf_var + n * (uint64_t)cfg->fill_size);
+  const uint64_t sizes[11] = {fin, unf_off, unf_var, cfg->fill_size, ntiles * nd * 8, (uint64_t)nf * nd * 16,
+                              (9 * m + 2 * npair) * 8, 2 * m * 4, n * 8, 8, rvar_max};
+  uint64_t need = 0;
+  for (uint64_t z : sizes) need += (std::max<uint64_t>(z, 16) + 255) & ~255ull;
+  if (need > c->dv_cap) {
+    HIP_OK(hipStreamSynchronize(s));
+    if (c->dv_arena) (void)hipFree(c->dv_arena);
+    c->dv_arena = nullptr;
+    c->dv_cap = 0;
+    if (hipMalloc(&c->dv_arena, need) != hipSuccess) return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+    c->dv_cap = need;
+  }
+  uint8_t* carve = c->dv_arena;
+  auto take = [&](uint64_t z) -> uint8_t* {
+    uint8_t* q = carve;
+    carve += (std::max<uint64_t>(z, 16) + 255) & ~255ull;
+    return q;
   };
-  struct Free {
-    std::vector<void*>& b;
-    ~Free() {
-      for (void* q : b) (void)hipFree(q);
-    }
-  } free_all{bufs};
-  uint8_t *d_in = nullptr, *d_off = nullptr, *d_var = nullptr, *d_fill = nullptr;
-  int64_t *d_start = nullptr, *d_dom = nullptr;
-  uint64_t* d_ptr = nullptr;  // unfilter tables for the 2m tiles, then per-pair tile tables
-  int32_t* d_st = nullptr;
-  uint64_t *d_roff = nullptr, *d_total = nullptr;
-  if (!dalloc((void**)&d_in, fin) || !dalloc((void**)&d_off, unf_off) || !dalloc((void**)&d_var, unf_var) ||
-      !dalloc((void**)&d_fill, cfg->fill_size) || !dalloc((void**)&d_start, ntiles * nd * 8) ||
-      !dalloc((void**)&d_dom, (uint64_t)nf * nd * 16) || !dalloc((void**)&d_ptr, (9 * m + 2 * npair) * 8) ||
-      !dalloc((void**)&d_st, 2 * m * 4) || !dalloc((void**)&d_roff, n * 8) || !dalloc((void**)&d_total, 8))
-    return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+  uint8_t* d_in = take(sizes[0]);
+  uint8_t* d_off = take(sizes[1]);
+  uint8_t* d_var = take(sizes[2]);
+  uint8_t* d_fill = take(sizes[3]);
+  int64_t* d_start = (int64_t*)take(sizes[4]);
+  int64_t* d_dom = (int64_t*)take(sizes[5]);
+  uint64_t* d_ptr = (uint64_t*)take(sizes[6]);  // unfilter tables for the 2m tiles, then per-pair tile tables
+  int32_t* d_st = (int32_t*)take(sizes[7]);
+  uint64_t* d_roff = (uint64_t*)take(sizes[8]);
+  uint64_t* d_total = (uint64_t*)take(sizes[9]);
+  uint8_t* const d_rvar_region = take(sizes[10]);
   // [2m in][2m in size][2m out][2m out size][m var size][npair offsets tile][npair var tile]
   std::vector<uint64_t> h(9 * m + 2 * npair, 0);
   uint64_t* hin = h.data();
@@ -2223,16 +2237,32 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
   uint64_t* hoff_t = hvsz + m;
   uint64_t* hvar_t = hoff_t + npair;
   uint64_t io = 0, oo = 0, ov = 0;
+  // host-to-device copies of adjacent host tiles coalesced (tiles read into
+  // one FilteredData-style block, filtered_data.h:152-644, are back to back
+  // in the order [offsets tile, var tile] per pair): one copy per run
+  const uint8_t* run_src = nullptr;
+  uint64_t run_dst = 0, run_len = 0;
+  auto h2d = [&](const uint8_t* src, uint64_t len) -> hipError_t {
+    hipError_t e = hipSuccess;
+    if (run_len && src == run_src + run_len) {
+      run_len += len;
+    } else {
+      if (run_len) e = hipMemcpyAsync(d_in + run_dst, run_src, run_len, hipMemcpyHostToDevice, s);
+      run_src = src;
+      run_dst = io;
+      run_len = len;
+    }
+    io += len;
+    return e;
+  };
   for (uint64_t k = 0; k < m; k++) {
     const uint64_t i = idx[k];
-    HIP_OK(hipMemcpyAsync(d_in + io, off_filtered[i], off_filtered_size[i], hipMemcpyHostToDevice, s));
     hin[k] = (uint64_t)(uintptr_t)(d_in + io);
+    HIP_OK(h2d(off_filtered[i], off_filtered_size[i]));
     hisz[k] = off_filtered_size[i];
-    io += off_filtered_size[i];
-    HIP_OK(hipMemcpyAsync(d_in + io, var_filtered[i], var_filtered_size[i], hipMemcpyHostToDevice, s));
     hin[m + k] = (uint64_t)(uintptr_t)(d_in + io);
+    HIP_OK(h2d(var_filtered[i], var_filtered_size[i]));
     hisz[m + k] = var_filtered_size[i];
-    io += var_filtered_size[i];
     hout[k] = (uint64_t)(uintptr_t)(d_off + oo);
     hosz[k] = (cells_per_tile + 1) * 8;
     hoff_t[i] = hout[k];
@@ -2243,6 +2273,7 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
     ov += var_unfiltered_size[i];
     hvsz[k] = var_unfiltered_size[i];
   }
+  if (run_len) HIP_OK(hipMemcpyAsync(d_in + run_dst, run_src, run_len, hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(d_ptr, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
   if (cfg->fill_size) HIP_OK(hipMemcpyAsync(d_fill, fill_value, cfg->fill_size, hipMemcpyHostToDevice, s));
   if (ntiles) HIP_OK(hipMemcpyAsync(d_start, tile_start, ntiles * nd * 8, hipMemcpyHostToDevice, s));
@@ -2318,8 +2349,8 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
   if (vbytes > var_cap || (vbytes && !result_var))
     return fail(TDBG_E_OUT_FULL, "dense var read: var buffer too small");
   if (vbytes) {
-    uint8_t* d_rvar = nullptr;
-    if (!dalloc((void**)&d_rvar, vbytes)) return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+    if (vbytes > rvar_max) return fail(TDBG_E_INTERNAL, "dense var read: result bound");
+    uint8_t* const d_rvar = d_rvar_region;  // (rvar_max bytes, carved above)
     rc = tdbg_dense_var_copy_async(c, &g, d_roff, d_total, d_rvar, s);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(result_var, d_rvar, vbytes, hipMemcpyDeviceToHost, s));

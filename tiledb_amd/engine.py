@@ -491,9 +491,13 @@ def dense_var_copy_async(ctx, fcfg, d_result_offsets, d_var_total, d_result_var,
 
 
 def dense_read_var_host(ctx, dp_off: DevicePipeline, dp_var: DevicePipeline, fcfg, tile_start, frag_dom,
-                        off_filtered, var_filtered, var_unfiltered_size, fill_value: bytes, var_cap: int):
+                        off_filtered, var_filtered, var_unfiltered_size, fill_value: bytes, var_cap: int,
+                        out_offsets=None, out_var=None):
     """tdbg_dense_read_var_host: host filtered offsets / var tiles per (tile,
-    fragment) (None: absent) -> (result offsets uint64, var bytes, statuses)."""
+    fragment) (None: absent) -> (result offsets uint64, var bytes, statuses).
+    out_offsets / out_var: optional caller result buffers (uint64 of the
+    subarray's cells, uint8 of var_cap bytes), written in place; the var
+    bytes are then returned as a view of out_var."""
     ntiles = len(tile_start)
     nf = fcfg.nfrag
     assert len(off_filtered) == ntiles * nf == len(var_filtered) == len(var_unfiltered_size)
@@ -509,8 +513,9 @@ def dense_read_var_host(ctx, dp_off: DevicePipeline, dp_var: DevicePipeline, fcf
     ncell = 1
     for d in range(fcfg.base.dim_num):
         ncell *= fcfg.base.sub_hi[d] - fcfg.base.sub_lo[d] + 1
-    roff = np.zeros(ncell, dtype=np.uint64)
-    rvar = np.zeros(max(var_cap, 1), dtype=np.uint8)
+    roff = out_offsets if out_offsets is not None else np.zeros(ncell, dtype=np.uint64)
+    rvar = out_var if out_var is not None else np.zeros(max(var_cap, 1), dtype=np.uint8)
+    assert roff.dtype == np.uint64 and roff.size >= ncell and rvar.dtype == np.uint8 and rvar.size >= max(var_cap, 1)
     total = ctypes.c_uint64()
     st = np.zeros(max(ntiles * nf, 1), dtype=np.int32)
     rc = lib.tdbg_dense_read_var_host(ctx.h, dp_off.h, dp_var.h, ctypes.byref(fcfg), ntiles, ts.ctypes.data,
@@ -520,8 +525,8 @@ def dense_read_var_host(ctx, dp_off: DevicePipeline, dp_var: DevicePipeline, fcf
                                       st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
     if rc and (rc in CALL_ERRORS or not st[:ntiles * nf].any()):
         _check(rc, "tdbg_dense_read_var_host")
-    return rc, roff, bytes(rvar[:int(total.value) * (fcfg.data_type_size if fcfg.elements_mode else 1)]), \
-        st[:ntiles * nf]
+    data = rvar[:int(total.value) * (fcfg.data_type_size if fcfg.elements_mode else 1)]
+    return rc, roff, (data if out_var is not None else bytes(data)), st[:ntiles * nf]
 
 
 def unfilter_cpu(dp: DevicePipeline, in_ptrs, in_size, out_ptrs, out_size, nthreads: int = 0,
