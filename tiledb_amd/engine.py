@@ -260,9 +260,25 @@ class Context:
         import torch
         return int(torch.cuda.current_stream().cuda_stream)
 
+    @staticmethod
+    def auto_chunk_parallel(dp: DevicePipeline, batch: TileBatch) -> bool:
+        """TDBG_CHUNK_PARALLEL when a tile holds more than one chunk (an
+        unfiltered size above the pipeline's max chunk size,
+        FilterPipeline::serialize's first u32; tile.cc:87-100): the chunk
+        directory then spreads the chunks over the GPU, where a tile-serial
+        launch decodes a tile's chunks one after another in one workgroup
+        (C5, 512 tiles of 4 MiB: 0.34 -> 0.46 of 8 TB/s, profiles/r05/c5big_ab.txt)."""
+        if batch.ntiles == 0 or len(dp.serialized) < 4:
+            return False
+        mc = int(np.frombuffer(dp.serialized[:4], dtype="<u4")[0]) or 65536
+        return bool(int(batch.out_size.max()) > mc)
+
     def unfilter(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
-                 stream=None, chunk_parallel: bool = False) -> np.ndarray:
-        """Synchronous unfilter; returns the per-tile status array."""
+                 stream=None, chunk_parallel=None) -> np.ndarray:
+        """Synchronous unfilter; returns the per-tile status array.
+        chunk_parallel: None = auto_chunk_parallel."""
+        if chunk_parallel is None:
+            chunk_parallel = self.auto_chunk_parallel(dp, batch)
         st = np.zeros(max(batch.ntiles, 1), dtype=np.int32)
         pin, psz, pout, posz = batch.ptrs()
         rc = lib.tdbg_unfilter_tiles_sync(
@@ -274,7 +290,9 @@ class Context:
         return st[: batch.ntiles]
 
     def unfilter_async(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
-                       stream=None, chunk_parallel: bool = False) -> None:
+                       stream=None, chunk_parallel=None) -> None:
+        if chunk_parallel is None:
+            chunk_parallel = self.auto_chunk_parallel(dp, batch)
         pin, psz, pout, posz = batch.ptrs()
         _check(lib.tdbg_unfilter_tiles_async(
             self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
