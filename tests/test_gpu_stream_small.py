@@ -392,6 +392,26 @@ def test_shuffle4_declined_tiles(eng, ctx, oracle_mod):
     assert ctx.stream_tiles() == s0
 
 
+@pytest.mark.parametrize("cfg", ["c3a", "c3b", "c4"])
+def test_small_every_chunk_size(eng, ctx, oracle_mod, cfg):
+    """C3a / C3b / C4 tiles of one chunk under 64 KiB (16 .. 8,190 u64
+    values: the last unit of two values half used, BWR / PD last windows
+    partial), mixed back to back: bit-exact, no fallback, and the streaming
+    kernel takes at least every tile of >= 1 KiB (tiles too small for its
+    256-B windows may go to the fused kernel)."""
+    rng = np.random.default_rng(71)
+    gen = W.c4_values if cfg == "c4" else W.c3_values
+    sizes = [128, 1024, 4000, 8192, 16000, 40000, 64000, 65520]
+    vals = [gen(k, rng)[: nb // 8] for k, nb in enumerate(sizes)]
+    ser, dt, cs, _, _ = W.config(cfg)
+    pipe = {"c3a": P(DD()), "c3b": P(RLE()), "c4": _pd_bwr()}[cfg]
+    case = Case(f"{cfg}_sizes", pipe, dt, cs, [as_u8(v) for v in vals])
+    enc, fused, fb, st = _run(eng, ctx, oracle_mod, case)
+    assert fb == 0
+    want_min = sum(e[2] >= 1024 for e in enc)
+    assert want_min <= st <= len(enc), (st, want_min, len(enc))
+
+
 def test_shuffle4_every_tile_size(eng, ctx, oracle_mod):
     """One-chunk [BYTESHUFFLE] int32 / uint32 tiles of every size class up to
     64 KiB (n = 4 .. 16,384 values, n mod 4 = 0..3: planes at every byte
@@ -418,8 +438,9 @@ def test_shuffle4_every_tile_size(eng, ctx, oracle_mod):
 def test_small_chunk_stream_multichunk(eng, ctx, oracle_mod, cfg):
     """Multi-chunk C3a / C3b / C4 tiles (16 chunks of 8,192 u64 values, the
     last one short) in a chunk-parallel launch: the small-image streaming
-    kernel takes every full chunk from the device chunk directory, the fused
-    kernel the short last ones; bit-exact vs the oracle."""
+    kernel takes every chunk -- the short last ones included -- of each tile
+    whose output starts 16-B aligned from the device chunk directory, the
+    fused kernel the other tiles' chunks; bit-exact vs the oracle."""
     from tests.test_gpu_parity import check_parity, encode
     rng = np.random.default_rng(77)
     gen = W.c4_values if cfg == "c4" else W.c3_values
@@ -435,11 +456,11 @@ def test_small_chunk_stream_multichunk(eng, ctx, oracle_mod, cfg):
     check_parity(eng, ctx, oracle_mod, case, [enc[i % 4][0] for i in range(n)], [enc[i % 4][2] for i in range(n)])
     f1, b1, _ = ctx.path_stats()
     assert b1 - b0 == 0 and f1 - f0 == n
-    # every full chunk of a tile whose output starts 16-B aligned (outputs
-    # packed back to back, TileBatch.from_packed; the streaming kernels'
-    # store rule), the rest by the fused kernel
+    # every chunk of a tile whose output starts 16-B aligned (outputs packed
+    # back to back, TileBatch.from_packed; the small kernel's store rule),
+    # the rest by the fused kernel
     osz = np.array([enc[i % 4][2] for i in range(n)], dtype=np.int64)
     off = np.concatenate([[0], np.cumsum(osz)[:-1]])
     aligned = int((off % 16 == 0).sum())
     assert 0 < aligned < n
-    assert ctx.stream_chunks() - c0 == 15 * aligned
+    assert ctx.stream_chunks() - c0 == 16 * aligned

@@ -141,7 +141,10 @@ __device__ __forceinline__ void dma(Lds<MODE>& L, const Desc& d) {
 // scratch: lanes [32 hh, 32 hh + 32) put their 8 units in row l & 31 (slot j
 // at j ^ (row & 7): conflict-free), then every store instruction writes 8
 // whole 128-B lines.  8 store instructions per call, every lane active.
-__device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[16], uint8_t* o, uint32_t l) {
+// Values vw + i (vw: the wave's first value of the round) at or past nv (a
+// chunk of nv < 8,192 values) are not stored: a 16-B unit holds two.
+__device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[16], uint8_t* o, uint32_t l,
+                                            uint32_t vw, uint32_t nv) {
 #pragma unroll
   for (int hh = 0; hh < 2; hh++) {
     __builtin_amdgcn_wave_barrier();
@@ -157,7 +160,10 @@ __device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[1
     for (int q = 0; q < 4; q++) {
       const uint32_t row = 8 * q + (l >> 3), sl = l & 7;
       const v4u y = *(const v4u*)(wsp + 4 * (8 * row + (sl ^ (row & 7))));
-      __builtin_nontemporal_store(y, (g_u4*)(o + 128u * (32u * hh + row) + 16u * sl));
+      const uint32_t vi = vw + 16u * (32u * hh + row) + 2u * sl;  // the unit's first value
+      uint8_t* const dst = o + 128u * (32u * hh + row) + 16u * sl;
+      if (vi + 2 <= nv) __builtin_nontemporal_store(y, (g_u4*)dst);
+      else if (vi < nv) *(uint2*)dst = make_uint2(y.x, y.y);
     }
   }
 }
@@ -328,7 +334,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
   // directory's scan kernel cleared it, and fbq is not passed here)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const uint32_t w = wave_();
-  uint64_t ok_tiles = 0;
+  uint64_t ok_tiles = 0, ok_bytes = 0;
   Desc cur{};
   bool cur_dma = false;
   bool stored = false;  // the last tile issued its 8 round-1 stores after the DMA
@@ -344,7 +350,12 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
   for (uint64_t j = blockIdx.x; j < ntl; j += G, it++) {
     const uint64_t jn = j + G;
     const uint32_t l = lane_();
-    bool ok = cur_dma && !(kp.flags & TDBG_TILE_OFFSETS) && cur.os == OUTB && (((uintptr_t)cur.out) & 15) == 0;
+    // a chunk of nv = os / 8 values, 16 <= nv <= 8,192 (short last chunks,
+    // tiles under 64 KiB: tile.cc:87-100)
+    bool ok = cur_dma && !(kp.flags & TDBG_TILE_OFFSETS) && cur.os >= 128 && cur.os <= OUTB && (cur.os & 7) == 0 &&
+              (((uintptr_t)cur.out) & 15) == 0;
+    // (uniform: scalar registers)
+    const uint32_t os = __builtin_amdgcn_readfirstlane((uint32_t)(ok ? cur.os : OUTB)), nv = os >> 3;
     Hdr hd{};
     Desc nxt{};
     bool nxt_dma = false;
@@ -373,13 +384,13 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
       const uint32_t nlo = c32(C, b), nhi = c32(C, b + 4), orig = c32(C, b + ho), fl = c32(C, b + ho + 4),
                      ml = c32(C, b + ho + 8);
       const uint32_t m = b + ho + 12;
-      ok = ok && (chunked || (nlo == 1 && nhi == 0)) && orig == OUTB && (uint64_t)ml + fl + ho + 12 <= cur.fs;
+      ok = ok && (chunked || (nlo == 1 && nhi == 0)) && orig == os && (uint64_t)ml + fl + ho + 12 <= cur.fs;
       hd.dst = m + ml;
       if constexpr (MODE == M_DD || MODE == M_RLE) {
         // compression frame (compression_filter.cc:413-486): 0 md parts, one
-        // data part of 65,536 bytes compressed to fl
+        // data part of os bytes compressed to fl
         const uint32_t nmd = c32(C, m), ndp = c32(C, m + 4), po = c32(C, m + 8), pc = c32(C, m + 12);
-        ok = ok && ml == 16 && nmd == 0 && ndp == 1 && po == OUTB && pc == fl;
+        ok = ok && ml == 16 && nmd == 0 && ndp == 1 && po == os && pc == fl;
         if constexpr (MODE == M_DD) {
           // [u8 bitsize][u64 n][u64 x0][u64 x1][u64 words] (dd_compressor.cc:314-345)
           const uint32_t s0 = hd.dst;
@@ -388,9 +399,9 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
           hd.x1 = c64(C, s0 + 17);
           hd.s = s0 + 25;
           hd.cb = bs + 1;
-          const uint32_t words = ((NV - 2) * hd.cb + 63) / 64;
+          const uint32_t words = ((nv - 2) * hd.cb + 63) / 64;
           // (bitsize <= 6: an 8,192-value stream of wider codes is bigger than CAP)
-          ok = ok && bs >= 1 && bs <= 6 && n0 == NV && n1 == 0 && fl == 25 + 8 * words;
+          ok = ok && bs >= 1 && bs <= 6 && n0 == nv && n1 == 0 && fl == 25 + 8 * words;
         } else {
           // runs of [u64 value][u8 len_hi][u8 len_lo] (rle_compressor.cc:103-141)
           hd.nr = fl / 10;
@@ -403,8 +414,9 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
         const uint32_t bo = c32(C, m), nw = c32(C, m + 4), ws = c32(C, m + 8 + 9);
         const uint32_t m2 = m + 8 + 13 * (nw < BWN ? nw : BWN);
         const uint32_t npw = c32(C, m2), wp = c32(C, m2 + 4 + 8);
-        ok = ok && bo == OUTB && nw >= 1 && nw <= BWN && ws >= 256 && (ws & (ws - 1)) == 0 && nw * ws == OUTB &&
-             npw >= 1 && npw <= PDN && wp >= 256 && wp <= 8192 && (wp & (wp - 1)) == 0 && npw * wp == OUTB &&
+        // (windows of ws / wp bytes, the last one holding the rest)
+        ok = ok && bo == os && nw >= 1 && nw <= BWN && ws >= 256 && (ws & (ws - 1)) == 0 && nw == (os + ws - 1) / ws &&
+             npw >= 1 && npw <= PDN && wp >= 256 && wp <= 8192 && (wp & (wp - 1)) == 0 && npw == (os + wp - 1) / wp &&
              ml == 8 + 13 * nw + 4 + 12 * npw;
         hd.bsh = ok ? 31 - __builtin_clz(ws) - 3 : 5;
         hd.psh = ok ? 31 - __builtin_clz(wp) - 3 : 7;
@@ -435,7 +447,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
           pre += (uint32_t)v2 < w ? x : 0u;
           tot += x;
         }
-        ok = ok && tot == NV;
+        ok = ok && tot == nv;
         uint32_t a = pre + inc - s4;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -459,14 +471,14 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
           mn = c64(C, e);
           const uint32_t bits = c8(C, e + 8), nb = c32(C, e + 9);
           const bool raw = bits >= 64 || (nb & 7) != 0;
-          bad = nb != wsz || (!raw && bits != 8 && bits != 16 && bits != 32);
+          bad = nb != (t + 1 < nw ? wsz : os - wsz * (nw - 1)) || (!raw && bits != 8 && bits != 16 && bits != 32);
           kind = raw ? 3u : bits == 8 ? 0u : bits == 16 ? 1u : 2u;
           cs = raw ? nb : (nb >> 3) << kind;
         }
         if (ok && t < npw) {
           const uint32_t e = hd.s + 4 + 12 * t;
           const uint64_t first = c64(C, e);
-          bad = bad || c32(C, e + 8) != psz;
+          bad = bad || c32(C, e + 8) != (t + 1 < npw ? psz : os - psz * (npw - 1));
           L.T.PT[t] = make_uint2((uint32_t)first, (uint32_t)(first >> 32));
         }
         const uint32_t inc = wave_incscan_u32(cs);
@@ -549,11 +561,11 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
               t += D;
               v[i] += t;
             }
-            stage_store(L.WS[w], v, obase, l);
+            stage_store(L.WS[w], v, obase, l, 4096 * h + 1024 * w, nv);
           }
         } else if constexpr (MODE == M_RLE) {
-          if (ok) {
-            const uint32_t c0 = 4096 * h + 1024 * w + 16 * l;
+          const uint32_t c0 = 4096 * h + 1024 * w + 16 * l;
+          if (ok && c0 < nv) {
             // the run holding c0 (a multiple of 16): one read of the
             // run-head scatter instead of a dependent binary search
             uint32_t r = L.T.HD[c0 >> 4];
@@ -561,7 +573,8 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
             uint64_t x = c64(L.C, hd.dst + 10 * r);
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-              if (c0 + k >= rend) {
+              // (cells past the chunk, nv not a multiple of 16: no run holds them)
+              if (c0 + k < nv && c0 + k >= rend) {
                 do {
                   r++;
                   rend = L.T.RS[r + 1];
@@ -575,14 +588,16 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
             lds_barrier();  // every wave is done with C
             next_dma();
           }
-          if (ok) stage_store(L.WS[w], v, obase, l);
+          if (ok) stage_store(L.WS[w], v, obase, l, 4096 * h + 1024 * w, nv);
         } else {  // M_PDBWR
           if (ok) {
             const uint32_t e0 = 4096 * h + 1024 * w + 16 * l;
-            const uint32_t wi = e0 >> hd.bsh;
+            // (lanes past a short chunk decode values no store takes, from
+            // the last windows)
+            const uint32_t wi = min(e0 >> hd.bsh, hd.nr - 1);
             const uint4 te = L.T.BT[wi];
             const uint64_t mn = ((uint64_t)te.w << 32) | te.z;
-            const uint32_t kind = te.y, j0 = e0 - (wi << hd.bsh);
+            const uint32_t kind = te.y, j0 = min(e0 - (wi << hd.bsh), (1u << hd.bsh) - 16);
             const uint32_t a = te.x + (j0 << (kind == 3 ? 3 : kind));
             // the lane's 16 deltas (BWR⁻¹: value + window minimum, wrapping)
             uint64_t d[16];
@@ -629,7 +644,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
               if (gl > 16) inc += dpp0<DPP_ROW_BCAST15, 0xa>(inc);
               if (gl > 32) inc += dpp0<DPP_ROW_BCAST31, 0xc>(inc);
             }
-            const uint2 f = L.T.PT[e0 >> hd.psh];
+            const uint2 f = L.T.PT[min(e0 >> hd.psh, hd.cb - 1)];
             const uint64_t base = (((uint64_t)f.y << 32) | f.x) + (inc - s);
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = base + d[k];
@@ -638,7 +653,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
             lds_barrier();  // every wave is done with C
             next_dma();
           }
-          if (ok) stage_store(L.WS[w], v, obase, l);
+          if (ok) stage_store(L.WS[w], v, obase, l, 4096 * h + 1024 * w, nv);
         }
       };
       round(std::integral_constant<uint32_t, 0>{});
@@ -653,6 +668,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
     if (!issued) next_dma();
     if (ok) {
       ok_tiles++;
+      ok_bytes += os;
       if (threadIdx.x == 0 && kp.status && !chunked) kp.status[cur.t] = TDBG_OK;
     }
     cur = nxt;
@@ -663,7 +679,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
   } else if (kp.stats && threadIdx.x == 0 && ok_tiles) {
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)(ok_tiles * OUTB));
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
     atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
   }
 }
