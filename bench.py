@@ -77,7 +77,9 @@ CONFIGS = {
 
 
 def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, device: int, seed: int,
-                align: int = 1, ctx=None, dp=None):
+                align: int = 1, ctx=None, dp=None, use_arena: bool = True):
+    """(use_arena: the batch lives on the run's one device arena -- so only
+    one such batch may be alive at a time; c3_combined keeps two)"""
     import workloads as W
 
     def encode(vals):
@@ -108,7 +110,8 @@ def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, devic
             packed[int(o):int(o) + pool_np[i].size] = pool_np[i]
     out_sizes = [vals[i].nbytes for i in idx]
     batch = engine.TileBatch.from_packed(packed, offs, sizes, out_sizes, device=device,
-                                         arena=bench_arena(engine, packed.size, int(sum(out_sizes)), device),
+                                         arena=(bench_arena(engine, packed.size, int(sum(out_sizes)), device)
+                                                if use_arena else None),
                                          in_first=bool(int(os.environ.get("TDBG_BENCH_IN_FIRST", "0"))),
                                          gap=int(os.environ.get("TDBG_BENCH_GAP", "0")))
     return batch, pool, vals, idx, packed, offs, sizes
@@ -403,7 +406,7 @@ def c3_combined(engine, ctx, W, args):
         dp = engine.DevicePipeline(ser, 23, int(dt), cs)
         batch, pool, vals, idx, packed, offs, sizes = build_batch(
             engine, c, "coords", CONFIGS[c]["tiles_per_gpu"], args.unique, torch.cuda.current_device(), seed=5,
-            ctx=ctx, dp=dp)
+            ctx=ctx, dp=dp, use_arena=False)
         if ctx.unfilter(dp, batch).any():
             raise SystemExit(f"{c}: first pass status nonzero")
         parts.append((c, dp, batch, vals, idx, float(sizes.sum()), float(sum(vals[i].nbytes for i in idx))))

@@ -143,8 +143,9 @@ __device__ __forceinline__ void dma(Lds<MODE>& L, const Desc& d) {
 // whole 128-B lines.  8 store instructions per call, every lane active.
 // Values vw + i (vw: the wave's first value of the round) at or past nv (a
 // chunk of nv < 8,192 values) are not stored: a 16-B unit holds two.
-__device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[16], uint8_t* o, uint32_t l,
-                                            uint32_t vw, uint32_t nv) {
+template <bool FULL>
+__device__ __forceinline__ void stage_store_(uint32_t* wsp, const uint64_t (&v)[16], uint8_t* o, uint32_t l,
+                                             uint32_t vw, uint32_t nv) {
 #pragma unroll
   for (int hh = 0; hh < 2; hh++) {
     __builtin_amdgcn_wave_barrier();
@@ -160,12 +161,22 @@ __device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[1
     for (int q = 0; q < 4; q++) {
       const uint32_t row = 8 * q + (l >> 3), sl = l & 7;
       const v4u y = *(const v4u*)(wsp + 4 * (8 * row + (sl ^ (row & 7))));
-      const uint32_t vi = vw + 16u * (32u * hh + row) + 2u * sl;  // the unit's first value
       uint8_t* const dst = o + 128u * (32u * hh + row) + 16u * sl;
-      if (vi + 2 <= nv) __builtin_nontemporal_store(y, (g_u4*)dst);
-      else if (vi < nv) *(uint2*)dst = make_uint2(y.x, y.y);
+      if (FULL) {  // (a whole 64 KiB chunk)
+        __builtin_nontemporal_store(y, (g_u4*)dst);
+      } else {
+        const uint32_t vi = vw + 16u * (32u * hh + row) + 2u * sl;  // the unit's first value
+        if (vi + 2 <= nv) __builtin_nontemporal_store(y, (g_u4*)dst);
+        else if (vi < nv) *(uint2*)dst = make_uint2(y.x, y.y);
+      }
     }
   }
+}
+
+__device__ __forceinline__ void stage_store(uint32_t* wsp, const uint64_t (&v)[16], uint8_t* o, uint32_t l,
+                                            uint32_t vw, uint32_t nv) {
+  if (nv == NV) stage_store_<true>(wsp, v, o, l, vw, nv);  // (uniform)
+  else stage_store_<false>(wsp, v, o, l, vw, nv);
 }
 
 // ---------------------------------------------------------------------------
@@ -571,17 +582,32 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
             uint32_t r = L.T.HD[c0 >> 4];
             uint32_t rend = L.T.RS[r + 1];
             uint64_t x = c64(L.C, hd.dst + 10 * r);
+            if (c0 + 16 <= nv) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-              // (cells past the chunk, nv not a multiple of 16: no run holds them)
-              if (c0 + k < nv && c0 + k >= rend) {
-                do {
-                  r++;
-                  rend = L.T.RS[r + 1];
-                } while (c0 + k >= rend);
-                x = c64(L.C, hd.dst + 10 * r);
+              for (int k = 0; k < 16; k++) {
+                if (c0 + k >= rend) {
+                  do {
+                    r++;
+                    rend = L.T.RS[r + 1];
+                  } while (c0 + k >= rend);
+                  x = c64(L.C, hd.dst + 10 * r);
+                }
+                v[k] = x;
               }
-              v[k] = x;
+            } else {
+              // (the one lane holding the chunk's end when nv is not a
+              // multiple of 16: no run holds the cells past it)
+#pragma unroll
+              for (int k = 0; k < 16; k++) {
+                if (c0 + k < nv && c0 + k >= rend) {
+                  do {
+                    r++;
+                    rend = L.T.RS[r + 1];
+                  } while (c0 + k >= rend);
+                  x = c64(L.C, hd.dst + 10 * r);
+                }
+                v[k] = x;
+              }
             }
           }
           if (h == 1) {

@@ -9,7 +9,7 @@ rows = []
 for f in glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True):
     rows += list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-k = [r for r in rows if "unfilter" in r["Kernel_Name"] or "fixup" in r["Kernel_Name"]]
+k = [r for r in rows if any(x in r["Kernel_Name"] for x in ("unfilter", "fixup", "dir_"))]
 last = k[-int(sys.argv[2]) if len(sys.argv) > 2 else -15:]
 prev = None
 for r in last:
