@@ -462,6 +462,8 @@ def kernel_name(cfgname, r):
         return "unfilter_c5tile_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname == "c1" and r["streamed"]:
         return "unfilter_shuffle4_kernel + unfilter_fused_kernel (queue of declined tiles)"
+    if cfgname in ("c2", "c2i") and r["streamed"]:
+        return "unfilter_c2tile_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname in ("c3a", "c3b", "c4") and r["streamed"]:
         return "unfilter_stream_small_kernel + unfilter_fused_kernel (queue of declined tiles)"
     return "unfilter_fused_kernel"

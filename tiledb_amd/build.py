@@ -35,6 +35,7 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
           ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
           ("tdbg_c5tile.hip", "tdbg_c5tile", []),
+          ("tdbg_c2tile.hip", "tdbg_c2tile", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
           ("tdbg_forward_stream.hip", "tdbg_forward_stream", []),
           ("tdbg_forward_small.hip", "tdbg_forward_small", []),
@@ -48,10 +49,11 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
 HOST_ONLY = {"tdbg_cpu.cpp"}
-NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip", "tdbg_c5tile.hip"}  # checked with -Rpass-analysis
+NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip", "tdbg_c5tile.hip",
+              "tdbg_c2tile.hip"}  # checked with -Rpass-analysis
 HEADERS = ["tdbg_desc.h", "tdbg_device.h", "tdbg_general.h", "tdbg_rules.h", "tdbg_stream_common.h", "tdbg_launch.h",
            "tdbg_hooks.h"]
-HOOK_UNITS = {"tdbg_host.cpp", "tdbg_io.cpp", "tdbg_c5tile.hip", "tdbg_stream.hip", "tdbg_stream_raw.hip",
+HOOK_UNITS = {"tdbg_host.cpp", "tdbg_io.cpp", "tdbg_c5tile.hip", "tdbg_c2tile.hip", "tdbg_stream.hip", "tdbg_stream_raw.hip",
               "tdbg_stream_small.hip"}
 
 

@@ -1,0 +1,375 @@
+// tdbg_c2tile.hip -- one-workgroup-per-tile unfilter kernel for BASELINE C2 /
+// C2i: [BITSHUFFLE] (+ BIT_WIDTH_REDUCTION, a pass-through on FLOAT32) and
+// [BITSHUFFLE, BIT_WIDTH_REDUCTION(256..4096)] on 4-byte integers, one 64 KiB
+// chunk per tile.
+//
+// The C5 tile kernel's shape (tdbg_c5tile.hip): a non-persistent
+// 1024-thread workgroup per tile, the launch's workgroups dealt so that each
+// XCD works through a contiguous eighth of the tiles; the whole filtered image
+// lands in LDS by LDS-DMA; wave 0 parses the prefix while the rest is in
+// flight:
+//   * the tile + chunk header (Tile::load_chunk_data, tile.cc:280-313);
+//   * C2i: the BWR metadata [u32 bytes][u32 nwin] + nwin x [i32 min][u8
+//     bits][u32 bytes] (bit_width_reduction_filter.cc:353-380; the window
+//     table is a DPP scan of the compressed sizes), then
+//   * the bitshuffle metadata [u32 1][u32 65536] (bitshuffle_filter.cc:
+//     128-167: one part, transformed in 8,192-B blocks).
+// Bitshuffle^-1
+// (bitshuffle_filter.cc:168-212): a block of 8,192 B is 32 bit rows of 256 B
+// (row 8 b + k = bit k of byte b of each of its 2,048 elements); wave w < 8
+// takes block w, lane t' its groups 4 t' .. 4 t' + 3 (elements 32 t' ..
+// 32 t' + 31): one dword per row holds the four groups' bytes (C2i: BWR^-1
+// on the way -- a 256-B row lies in one window, so the row's read is one
+// wave-uniform 8-bit / 16-bit / raw decode from the compressed window), two 4x4 byte
+// transposes per byte plane give each group's 8x8 bit matrix, transpose8x8
+// the 8 elements' byte, two more 4x4 transposes the elements.  The elements
+// go back to LDS (XOR-swizzled 16-B units, after a barrier) and leave as
+// lane-consecutive 16-B stores, 1 KiB per wave instruction (outputs 4-B
+// aligned).
+//
+// Other shapes (sizes, windows, more parts, malformed, offsets tiles) are
+// queued for the fused kernel, which runs on the queue in the same launch.
+// Nothing is written to a tile's output before all its checks passed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/tiledb_amd.h"
+#include "tdbg_desc.h"
+#include "tdbg_device.h"
+#include "tdbg_launch.h"
+#include "tdbg_stream_common.h"
+#include "tdbg_hooks.h"
+
+namespace tdbg {
+namespace c2t {
+
+using namespace sc;
+
+constexpr int NT = 1024;
+constexpr uint32_t OUTB = 65536;
+constexpr uint32_t IMGU = 4256;  // 16-B units of the image stage (68,096 B)
+constexpr uint32_t IMG_CAP = IMGU * 16 - 15;
+constexpr uint32_t TABN = 320;
+constexpr uint32_t OFFM = (1u << 20) - 1;
+constexpr uint32_t GRID_CAP = 1u << 22;
+constexpr uint32_t PFX = 192;  // 16-B units of the image prefix the parse reads (3 KiB)
+
+struct Lds {
+  uint32_t IMG[IMGU * 4];
+  uint2 TAB[TABN];  // BWR window: {image offset of its data | kind << 20, minimum}
+  uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, image byte of the bitshuffled data
+};
+
+// a 16-B unit at a 4-B aligned address (global_store_dwordx4 needs no more)
+typedef uint32_t v4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) v4a g_a4;
+
+__device__ __forceinline__ uint32_t rd32(const uint32_t* a, uint32_t o) {
+  return __builtin_amdgcn_alignbyte(a[(o >> 2) + 1], a[o >> 2], o & 3);
+}
+
+template <bool SGN>
+__device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
+  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
+}
+
+__device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
+  if (threadIdx.x == 0) {
+    const uint32_t k = atomicAdd(kp.sq, 1u);
+    if (k < kp.sq_cap) kp.sq[1 + k] = (uint32_t)t;
+    else if (kp.status) kp.status[t] = TDBG_E_INTERNAL;
+  }
+}
+
+// MODE 0: [BITSHUFFLE] (a FLOAT32 BWR is a pass-through with no metadata,
+// bit_width_reduction_filter.cc:166-176); MODE 1: [BITSHUFFLE, BWR] on 4-byte
+// integers.  One wave.
+template <int MODE>
+__device__ __forceinline__ void parse(Lds& L, uint32_t b, uint64_t fs, uint32_t l) {
+  const uint32_t* P = L.IMG;
+  const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + 8), fl = rd32(P, b + 12),
+                 ml = rd32(P, b + 16);
+  const uint32_t m = b + 20;
+  bool ok = nlo == 1 && nhi == 0 && orig == OUTB && (uint64_t)ml + fl + 20 <= fs;
+  if (MODE == 0) {
+    ok = ok && ml == 8 && fl == OUTB && rd32(P, m) == 1 && rd32(P, m + 4) == OUTB;
+    if (l == 0) {
+      L.hd[0] = ok ? 1u : 0u;
+      L.hd[3] = m + 8;
+    }
+    return;
+  }
+  // BWR md; lane l: windows 5 l .. 5 l + 4 (45 bytes from e0)
+  const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4), ws = rd32(P, m + 13);
+  ok = ok && Lb == OUTB && nwr >= 1 && nwr <= TABN && ml == 8 + 9 * nwr + 8 && ws >= 256 && ws <= 4096 &&
+       (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwr;
+  const uint32_t nwin = ok ? nwr : 1;
+  const uint32_t e0 = m + 8 + 45 * l;
+  uint32_t R[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) R[k] = P[(e0 >> 2) + k];
+  const uint32_t sh = e0 & 3;
+  auto rw = [&](int o) -> uint32_t {
+    const uint32_t lo0 = R[o >> 2], hi0 = R[(o >> 2) + 1], hi1 = R[(o >> 2) + 2];
+    const uint32_t s = sh + (uint32_t)(o & 3);
+    return s < 4 ? __builtin_amdgcn_alignbyte(hi0, lo0, s) : __builtin_amdgcn_alignbyte(hi1, hi0, s - 4);
+  };
+  uint32_t cs[5], kind[5], mn[5];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint32_t wi = 5 * l + q;
+    const uint32_t vmin = rw(9 * q), bits = rw(9 * q + 4) & 0xffu, nb = rw(9 * q + 5);
+    const bool in = wi < nwin;
+    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+    bad = bad || (in && nb != want);
+    const bool raw = bits >= 32 || (nb & 3) != 0;
+    bad = bad || (in && !raw && bits != 8 && bits != 16);
+    kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
+    cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+    mn[q] = raw ? 0 : vmin;
+  }
+  const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
+  const uint32_t inc = wave_incscan_u32(s5);
+  ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
+  const uint32_t dst = 20 + ml;  // image offset (from b) of the BWR data
+  {
+    uint32_t off = dst + inc - s5;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kind[q] << 20), mn[q]);
+      off += cs[q];
+    }
+  }
+  // the bitshuffle md after the windows' headers
+  const uint32_t f = m + 8 + 9 * nwin;
+  ok = ok && rd32(P, f) == 1 && rd32(P, f + 4) == OUTB;
+  if (l == 0) {
+    L.hd[0] = ok ? 1u : 0u;
+    L.hd[1] = 31 - __builtin_clz(ws);
+    L.hd[2] = nwin - 1;
+    L.hd[3] = 0;  // (the stream is decoded to LDS byte 0)
+  }
+}
+
+// (A/B, experiments build) BWR^-1 of the 64 KiB stream into LDS, in place
+// over the image, as a pass of its own: thread T
+// decodes 16-B units T + 1024 j (four elements, one window), per round one
+// wave-uniform decoder (all-8-bit: one dword; else per element by kind)
+template <bool SGN>
+__device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w,
+                                                uint32_t l) {
+  v4u dv[4];
+  uint2 te[4];
+  uint32_t ea[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t e = 4 * (1024 * j + 64 * w + l);
+    uint32_t W = e >> esh;
+    W = W < wlast ? W : wlast;
+    te[j] = L.TAB[W];
+    const uint32_t kind = te[j].x >> 20;
+    ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);
+  }
+  uint32_t D[4][5];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t* p = L.IMG + (ea[j] >> 2);
+#pragma unroll
+    for (int k = 0; k < 5; k++) D[j][k] = p[k];
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
+    if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
+      const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
+      dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
+    } else {
+      const uint32_t r0 = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh), r1 = __builtin_amdgcn_alignbyte(D[j][2], D[j][1], sh);
+      const uint32_t r2 = __builtin_amdgcn_alignbyte(D[j][3], D[j][2], sh), r3 = __builtin_amdgcn_alignbyte(D[j][4], D[j][3], sh);
+      const bool b8 = kind == 0, raw = kind == 2;
+      const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
+      const uint32_t e1 = ext<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
+      const uint32_t e2 = ext<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
+      const uint32_t e3 = ext<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
+      dv[j] = v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
+    }
+  }
+  lds_barrier();  // every compressed byte is in registers
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+}
+
+__device__ __forceinline__ void tr4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t (&o)[4]) {
+  const uint32_t a = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
+  const uint32_t b = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
+  const uint32_t c = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+  const uint32_t d = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+  o[0] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+  o[1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+  o[2] = __builtin_amdgcn_perm(d, c, 0x05040100u);
+  o[3] = __builtin_amdgcn_perm(d, c, 0x07060302u);
+}
+
+// 16-B unit u of the output at its XOR-swizzled LDS slot (the eight b128
+// writes of a lane land in distinct bank groups)
+__device__ __forceinline__ uint32_t uslot(uint32_t u) { return u ^ ((u >> 3) & 7u); }
+
+template <int MODE, bool SGN, bool MAT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+unfilter_c2tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
+  __shared__ Lds L;
+  const uint32_t w = wave_(), l = lane_();
+  const uint32_t n8 = (cnt + 7) >> 3;
+  const uint32_t j = (blockIdx.x & 7) * n8 + (blockIdx.x >> 3);
+  if (j >= cnt) return;
+  const uint64_t t = (uint64_t)base + j;
+  if (t >= kp.ntiles) return;
+  if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
+  const uint64_t fs = kp.in_size[t];
+  const uint8_t* in = kp.in[t];
+  uint8_t* out = kp.out[t];
+  if ((kp.flags & TDBG_TILE_OFFSETS) || kp.chunks || kp.out_size[t] != OUTB || (((uintptr_t)out) & 3) || fs > IMG_CAP ||
+      fs < 28 + 8) {
+    decline(kp, t);
+    return;
+  }
+  const uint32_t b = (uint32_t)((uintptr_t)in & 15);
+  {
+    const uint64_t a0 = (uint64_t)in & ~15ull;
+    const uint32_t nu = (uint32_t)((b + fs + 15) >> 4);
+    if (w == 0) {
+#pragma unroll
+      for (uint32_t k = 0; k < PFX / 64; k++)
+        if (64 * k < nu && 64 * k + l < nu) dma16(a0 + 16ull * (64 * k + l), lds_addr(L.IMG) + 1024 * k);
+    }
+    uint32_t after = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < (IMGU - PFX + NT - 1) / NT; i++) {
+      const uint32_t u0 = PFX + 64 * (w + 16 * i);
+      if (u0 < nu) {
+        after++;
+        if (u0 + l < nu) dma16(a0 + 16ull * (u0 + l), lds_addr(L.IMG) + 16 * u0);
+      }
+    }
+    if (w == 0) {
+      switch (__builtin_amdgcn_readfirstlane(after)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      }
+      __builtin_amdgcn_s_setprio(3);
+      parse<MODE>(L, b, fs, l);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  if (__builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
+    decline(kp, t);
+    return;
+  }
+  uint32_t S = __builtin_amdgcn_readfirstlane(L.hd[3]);
+  const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]), wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
+  if (MODE == 1 && MAT) {
+    bwr_materialize<SGN>(L, b, wsh - 2, wlast, w, l);
+    lds_barrier();  // the bitshuffled stream at LDS byte 0
+  }
+  // bitshuffle^-1: wave w < 8 takes block w (8,192 B), lane l its groups
+  // 4 l .. 4 l + 3
+  uint32_t E[4][8];
+  if (w < 8) {
+    const uint32_t rb = S + 8192 * w + 4 * l;
+    // row r's dword of lane l.  C2i: decoded from its BWR window on the way
+    // (a 256-B row is one window or part of one: a wave-uniform decoder)
+    auto row = [&](uint32_t r) -> uint32_t {
+      if (MODE == 0 || MAT) return (S & 3) == 0 ? L.IMG[(rb + r * 256) >> 2] : rd32(L.IMG, rb + r * 256);
+      const uint32_t o = 8192 * w + 256 * r;
+      uint32_t W = o >> wsh;
+      W = W < wlast ? W : wlast;
+      const uint2 te = L.TAB[W];
+      const uint32_t kind = te.x >> 20;
+      const uint32_t x = rd32(L.IMG, (te.x & OFFM) + b + ((((o - (W << wsh)) >> 2) + l) << kind));
+      return kind == 2 ? x : ext<SGN>(x, 0, 8u << kind) + te.y;
+    };
+    uint64_t y[4][4];  // [group][byte plane]
+#pragma unroll
+    for (int pb = 0; pb < 4; pb++) {
+      uint32_t Dr[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) Dr[k] = row(8 * pb + k);
+      uint32_t lo[4], hi[4];
+      tr4(Dr[0], Dr[1], Dr[2], Dr[3], lo);
+      tr4(Dr[4], Dr[5], Dr[6], Dr[7], hi);
+#pragma unroll
+      for (int g = 0; g < 4; g++) y[g][pb] = transpose8x8(((uint64_t)hi[g] << 32) | lo[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      uint32_t e0[4], e1[4];
+      tr4((uint32_t)y[g][0], (uint32_t)y[g][1], (uint32_t)y[g][2], (uint32_t)y[g][3], e0);
+      tr4((uint32_t)(y[g][0] >> 32), (uint32_t)(y[g][1] >> 32), (uint32_t)(y[g][2] >> 32), (uint32_t)(y[g][3] >> 32),
+          e1);
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        E[g][m] = e0[m];
+        E[g][4 + m] = e1[m];
+      }
+    }
+  }
+  lds_barrier();  // every row read before the elements overwrite them
+  if (w < 8) {
+    // lane bytes [8192 w + 128 l, +128) = units 512 w + 8 l + i
+    const uint32_t u0 = 512 * w + 8 * l;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      *(v4u*)(L.IMG + 4 * uslot(u0 + i)) =
+          v4u{E[i >> 1][4 * (i & 1)], E[i >> 1][4 * (i & 1) + 1], E[i >> 1][4 * (i & 1) + 2], E[i >> 1][4 * (i & 1) + 3]};
+  }
+  lds_barrier();
+  const uint32_t T = 64 * w + l;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++) {
+    const uint32_t u = 1024 * r + T;
+    const v4u v = *(const v4u*)(L.IMG + 4 * uslot(u));
+    __builtin_nontemporal_store((v4a)v, (g_a4*)(out + 16 * u));
+  }
+  if (threadIdx.x == 0) {
+    if (kp.status) kp.status[t] = TDBG_OK;
+    if (kp.stats) {
+      uint64_t* s = kp.stats + TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63));
+      atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
+      atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)OUTB);
+      atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
+    }
+  }
+}
+
+}  // namespace c2t
+}  // namespace tdbg
+
+// mode 0: [BITSHUFFLE] / [BITSHUFFLE, BWR pass-through]; 1: [BITSHUFFLE, BWR]
+// on 4-byte integers (sgn: signed).  One workgroup per tile, launches of at
+// most GRID_CAP tiles.
+extern "C" hipError_t tdbg_launch_c2tile(const tdbg::KParams* kp, int mode, int sgn, hipStream_t s) {
+  using namespace tdbg::c2t;
+#ifdef TDBG_EXPERIMENTS
+  static const bool mat = tdbg_hook("TDBG_C2T_MAT") != nullptr;  // A/B: BWR^-1 as its own LDS pass
+#else
+  constexpr bool mat = false;
+#endif
+  auto k = mode == 0 ? unfilter_c2tile_kernel<0, false, false>
+           : mat     ? (sgn ? unfilter_c2tile_kernel<1, true, true> : unfilter_c2tile_kernel<1, false, true>)
+                     : (sgn ? unfilter_c2tile_kernel<1, true, false> : unfilter_c2tile_kernel<1, false, false>);
+  for (uint64_t b = 0; b < kp->ntiles; b += GRID_CAP) {
+    const uint32_t cnt = (uint32_t)std::min<uint64_t>(kp->ntiles - b, GRID_CAP);
+    TDBG_LAUNCH(k, dim3(8 * ((cnt + 7) / 8)), dim3(NT), s, *kp, (uint32_t)b, cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}

@@ -67,6 +67,7 @@ extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
 extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s);
+extern "C" hipError_t tdbg_launch_c2tile(const tdbg::KParams* kp, int mode, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                hipStream_t s);
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
@@ -712,7 +713,16 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
                          : ((P.fast == 15 || P.fast == 16) && P.nstages == 2 && P.s[0].w == 8 &&
                             P.s[0].dts == 8 && P.s[1].w == 8 && P.s[1].dts == 8)               ? 2
                                                                                                : -1;
-  const bool streamed = queued && !chunked && !d_list && !no_stream && (c5_stream || small_mode >= 0 || shuffle4);
+  // C2 [BITSHUFFLE] (+ a pass-through stage) and C2i [BITSHUFFLE, BWR] on
+  // 4-byte values: the one-workgroup-per-tile kernel (tdbg_c2tile.hip),
+  // 0 / 1; -1 none
+  static const bool no_c2tile = tdbg_hook("TDBG_NO_C2TILE") != nullptr;  // A/B: the fused kernel alone
+  const int c2_mode = (no_c2tile || chunked || P.fast == 0 || P.s[0].kind != TDBG_K_BITSHUFFLE || P.s[0].w != 4) ? -1
+                      : (P.nstages == 1 || (P.nstages == 2 && P.s[1].kind == TDBG_K_PASS))            ? 0
+                      : (P.nstages == 2 && P.s[1].kind == TDBG_K_BWR && P.s[1].w == 4 && P.s[1].dts == 4) ? 1
+                                                                                                          : -1;
+  const bool streamed =
+      queued && !chunked && !d_list && !no_stream && (c5_stream || small_mode >= 0 || shuffle4 || c2_mode >= 0);
   // The fallback queue starts empty for this launch, whatever ran before on
   // any stream: a memset, or in a streamed launch the streaming kernel's first
   // thread (it runs before the fused kernel that appends).  The streaming
@@ -838,6 +848,9 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
     if (shuffle4) {
       if (!skip_fused) e = tdbg_launch_stream_shuffle4(&ks, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("shuffle stream kernel launch: ") + hipGetErrorString(e));
+    } else if (c2_mode >= 0) {
+      if (!skip_fused) e = tdbg_launch_c2tile(&ks, c2_mode, c2_mode == 1 && P.s[1].sgn ? 1 : 0, stream);
+      if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("bitshuffle tile kernel launch: ") + hipGetErrorString(e));
     } else if (small_mode >= 0) {
       const int sgn = (small_mode == 2 && P.s[1].sgn) ? 1 : 0;
       if (!skip_fused)

@@ -13,8 +13,8 @@ import sys
 PEAK = 8000.0
 
 
-KERNELS = ("unfilter_stream", "unfilter_c5tile", "unfilter_shuffle4", "unfilter_fused_kernel")
-STARTS = ("unfilter_stream_kernel", "unfilter_c5tile_kernel", "unfilter_stream_small_kernel", "unfilter_shuffle4_kernel")
+KERNELS = ("unfilter_stream", "unfilter_c5tile", "unfilter_c2tile", "unfilter_shuffle4", "unfilter_fused_kernel")
+STARTS = ("unfilter_stream_kernel", "unfilter_c5tile_kernel", "unfilter_c2tile_kernel", "unfilter_stream_small_kernel", "unfilter_shuffle4_kernel")
 
 
 def _launches(items):
