@@ -20,9 +20,11 @@
 // takes block w, lane t' its groups 4 t' .. 4 t' + 3 (elements 32 t' ..
 // 32 t' + 31): one dword per row holds the four groups' bytes (C2i: BWR^-1
 // on the way -- a 256-B row lies in one window, so the row's read is one
-// wave-uniform 8-bit / 16-bit / raw decode from the compressed window), two 4x4 byte
-// transposes per byte plane give each group's 8x8 bit matrix, transpose8x8
-// the 8 elements' byte, two more 4x4 transposes the elements.  The elements
+// wave-uniform 8-bit / 16-bit / raw decode from the compressed window).  Per
+// byte plane, three bit-swap stages across the plane's eight row registers
+// transpose the four groups' 8x8 bit matrices at once (72 VALU operations for
+// 4 matrices); a 4x4 byte transpose per element index then assembles the
+// elements.  The elements
 // go back to LDS (XOR-swizzled 16-B units, after a barrier) and leave as
 // lane-consecutive 16-B stores, 1 KiB per wave instruction (outputs 4-B
 // aligned).
@@ -291,34 +293,45 @@ unfilter_c2tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       const uint32_t o = 8192 * w + 256 * r;
       uint32_t W = o >> wsh;
       W = W < wlast ? W : wlast;
-      const uint2 te = L.TAB[W];
-      const uint32_t kind = te.x >> 20;
-      const uint32_t x = rd32(L.IMG, (te.x & OFFM) + b + ((((o - (W << wsh)) >> 2) + l) << kind));
-      return kind == 2 ? x : ext<SGN>(x, 0, 8u << kind) + te.y;
+      const uint2 tv = L.TAB[W];
+      const uint32_t tx = __builtin_amdgcn_readfirstlane(tv.x), mn = __builtin_amdgcn_readfirstlane(tv.y);
+      const uint32_t kind = tx >> 20;  // (scalar: the row's decoder is a wave-uniform branch)
+      const uint32_t x = rd32(L.IMG, (tx & OFFM) + b + (((o - (W << wsh)) >> 2) << kind) + (l << kind));
+      return kind == 2 ? x : ext<SGN>(x, 0, 8u << kind) + mn;
     };
-    uint64_t y[4][4];  // [group][byte plane]
+    // Per byte plane pb: rows 8 pb + k (k = 0..7) in R[pb][k], byte g of
+    // each = group g's 8x8 bit matrix (row k, bit e = element e).  Three
+    // swap stages across the eight registers (blocks of 4, 2, 1 bits)
+    // transpose the four matrices at once: R[pb][e] byte g = byte pb of
+    // element 8 g + e.  One 4x4 byte transpose per e then assembles the
+    // elements.
+    uint32_t R[4][8];
+    auto sw = [](uint32_t& x, uint32_t& z, int sh, uint32_t m) {
+      const uint32_t t = ((x >> sh) ^ z) & m;
+      z ^= t;
+      x ^= t << sh;
+    };
 #pragma unroll
     for (int pb = 0; pb < 4; pb++) {
-      uint32_t Dr[8];
+      uint32_t* D = R[pb];
 #pragma unroll
-      for (int k = 0; k < 8; k++) Dr[k] = row(8 * pb + k);
-      uint32_t lo[4], hi[4];
-      tr4(Dr[0], Dr[1], Dr[2], Dr[3], lo);
-      tr4(Dr[4], Dr[5], Dr[6], Dr[7], hi);
+      for (int k = 0; k < 8; k++) D[k] = row(8 * pb + k);
 #pragma unroll
-      for (int g = 0; g < 4; g++) y[g][pb] = transpose8x8(((uint64_t)hi[g] << 32) | lo[g]);
+      for (int k = 0; k < 4; k++) sw(D[k], D[k + 4], 4, 0x0F0F0F0Fu);
+#pragma unroll
+      for (int k = 0; k < 8; k += 4) {
+        sw(D[k], D[k + 2], 2, 0x33333333u);
+        sw(D[k + 1], D[k + 3], 2, 0x33333333u);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) sw(D[k], D[k + 1], 1, 0x55555555u);
     }
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      uint32_t e0[4], e1[4];
-      tr4((uint32_t)y[g][0], (uint32_t)y[g][1], (uint32_t)y[g][2], (uint32_t)y[g][3], e0);
-      tr4((uint32_t)(y[g][0] >> 32), (uint32_t)(y[g][1] >> 32), (uint32_t)(y[g][2] >> 32), (uint32_t)(y[g][3] >> 32),
-          e1);
+    for (int e = 0; e < 8; e++) {
+      uint32_t o[4];
+      tr4(R[0][e], R[1][e], R[2][e], R[3][e], o);
 #pragma unroll
-      for (int m = 0; m < 4; m++) {
-        E[g][m] = e0[m];
-        E[g][4 + m] = e1[m];
-      }
+      for (int g = 0; g < 4; g++) E[g][e] = o[g];
     }
   }
   lds_barrier();  // every row read before the elements overwrite them
