@@ -37,6 +37,7 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           ("tdbg_c5tile.hip", "tdbg_c5tile", []),
           ("tdbg_c2tile.hip", "tdbg_c2tile", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
+          ("tdbg_stream_small.hip", "tdbg_stream_small_512", ["-DTDBG_SMALL_NT=512"]),
           ("tdbg_forward_stream.hip", "tdbg_forward_stream", []),
           ("tdbg_forward_small.hip", "tdbg_forward_small", []),
           ("tdbg_forward_shuffle.hip", "tdbg_forward_shuffle", []),

@@ -47,8 +47,10 @@ struct Batch {
 // descriptor is one chunk: its image starts at the chunk's 12-byte header
 // ([u32 orig][u32 filtered][u32 md], tile.cc:280-313) and its output at the
 // chunk's offset in the tile's buffer.
-__device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl) {
-  const uint64_t j = blockIdx.x + (base + (threadIdx.x & 63)) * (uint64_t)gridDim.x;
+// (bid: the workgroup's index in the launch's deal of work items; blockIdx.x
+// unless a kernel remaps it)
+__device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl, uint32_t bid) {
+  const uint64_t j = bid + (base + (threadIdx.x & 63)) * (uint64_t)gridDim.x;
   Batch b{0, 0, 0, 0};
   if (j < ntl) {
     if (kp.chunks) {
@@ -67,6 +69,9 @@ __device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, ui
     }
   }
   return b;
+}
+__device__ __forceinline__ Batch batch_load(const KParams& kp, uint64_t base, uint64_t ntl) {
+  return batch_load(kp, base, ntl, blockIdx.x);
 }
 
 // work items of a launch: tiles, or (chunk mode / a queue) a device count

@@ -46,6 +46,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "../../include/tiledb_amd.h"
@@ -55,18 +56,38 @@
 #include "tdbg_stream_common.h"
 #include "tdbg_hooks.h"
 
+// Built twice (tiledb_amd/build.py): TDBG_SMALL_NT 256 -- the persistent
+// kernel, two rounds of 4,096 values per tile, 4-5 workgroups per CU -- and
+// 512 -- one workgroup per tile (non-persistent, the launch's workgroups
+// dealt XCD-contiguously as in tdbg_c5tile.hip), one round of 8,192 values.
+#ifndef TDBG_SMALL_NT
+#define TDBG_SMALL_NT 256
+#endif
+#if TDBG_SMALL_NT == 256
+#define TDBG_SSM_NS ssm
+#define TDBG_SSM_SYM(x) x
+#elif TDBG_SMALL_NT == 512
+#define TDBG_SSM_NS ssm512
+#define TDBG_SSM_SYM(x) x##_512
+#else
+#error "TDBG_SMALL_NT: 256 or 512"
+#endif
+
 namespace tdbg {
-namespace ssm {
+namespace TDBG_SSM_NS {
 
 using namespace sc;
 
-constexpr int NT = 256;  // 4 wave64 per workgroup
-constexpr int NWV = NT / 64;
+constexpr int NT = TDBG_SMALL_NT;
+constexpr int NWV = NT / 64;      // waves per workgroup
+constexpr bool NP = NT == 512;    // one tile per workgroup, XCD-contiguous deal
+constexpr uint32_t NR = 8 / NWV;  // rounds of 1,024 NWV values per tile
 constexpr uint32_t OUTB = 65536;   // output bytes per tile
 constexpr uint32_t NV = OUTB / 8;  // 8-byte values per tile
 constexpr uint32_t CPAD = 128;     // reads past the image stay inside C
 constexpr uint32_t WSD = 1024;     // scratch dwords per wave (4 KiB)
-constexpr uint32_t RUNCAP = 1024;  // RLE runs per tile (4 per thread)
+constexpr uint32_t RUNCAP = 1024;  // RLE runs per tile
+constexpr uint32_t RPT = RUNCAP / NT;  // runs per thread
 constexpr uint32_t BWN = 256;      // BWR windows per tile (>= 256 B each)
 constexpr uint32_t PDN = 256;      // PD windows per tile (>= 256 B each)
 
@@ -81,7 +102,7 @@ template <int MODE>
 struct Tab;
 template <>
 struct Tab<M_DD> {
-  uint64_t red[2][NWV][2];  // per round and wave: DD aggregate (A, B)
+  uint64_t red[NR][NWV][2];  // per round and wave: DD aggregate (A, B)
 };
 template <>
 struct Tab<M_RLE> {
@@ -302,21 +323,23 @@ __device__ __forceinline__ uint64_t bwr_ext(uint64_t x, uint32_t kind) {
 // ---------------------------------------------------------------------------
 // workgroups per CU by LDS (24.5 / 28.6 / 38.6 KB); the register budget
 // follows (80 / 96 / 128 VGPRs)
+// (512 threads: 41 / 46 / 55 KB; 2 per CU -- 3 would need <= 80 VGPRs, and
+// DD / RLE then spill)
 template <int MODE>
 struct Occ {
-  static constexpr int v = MODE == M_DD ? 5 : MODE == M_RLE ? 5 : 4;
+  static constexpr int v = NP ? 2 : (MODE == M_DD ? 5 : MODE == M_RLE ? 5 : 4);
 };
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
 // base + i) for the fused kernel.  Wave 0.
-__device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, uint32_t base) {
+__device__ __forceinline__ void queue_batch(const KParams& kp, uint64_t mask, uint32_t base, uint32_t bid) {
   const uint32_t l = threadIdx.x & 63;
   uint32_t b0 = 0;
   if (l == 0) b0 = atomicAdd(kp.sq, (uint32_t)__builtin_popcountll(mask));
   b0 = __builtin_amdgcn_readfirstlane(b0);
   if ((mask >> l) & 1) {
     const uint32_t k = b0 + (uint32_t)__builtin_popcountll(mask & ((1ull << l) - 1));
-    const uint32_t t = (uint32_t)(blockIdx.x + (uint64_t)(base + l) * gridDim.x);
+    const uint32_t t = (uint32_t)(bid + (uint64_t)(base + l) * gridDim.x);
     if (k < kp.sq_cap) kp.sq[1 + k] = t;
     else if (kp.status) kp.status[kp.chunks ? kp.chunks[t].tile : t] = TDBG_E_INTERNAL;
   }
@@ -344,21 +367,25 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
   // next on the same stream and is the only one to append; chunk mode: the
   // directory's scan kernel cleared it, and fbq is not passed here)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
+  // the workgroup's place in the deal: NP, workgroups are dealt over the 8
+  // XCDs round-robin, so XCD x takes the contiguous eighth [x G / 8, +G / 8)
+  // of the items (G a multiple of 8; a placement assumption for speed only)
+  const uint32_t bid = NP ? (blockIdx.x & 7) * (uint32_t)(G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t w = wave_();
   uint64_t ok_tiles = 0, ok_bytes = 0;
   Desc cur{};
   bool cur_dma = false;
   bool stored = false;  // the last tile issued its 8 round-1 stores after the DMA
   Batch bt{0, 0, 0, 0};
-  if (blockIdx.x < ntl) {
-    bt = batch_load(kp, 0, ntl);
-    cur = batch_get(bt, 0, blockIdx.x);
+  if (bid < ntl) {
+    bt = batch_load(kp, 0, ntl, bid);
+    cur = batch_get(bt, 0, bid);
     cur_dma = fits<MODE>(cur);
     if (cur_dma) dma(L, cur);
   }
   uint64_t dmask = 0;
   uint32_t it = 0;
-  for (uint64_t j = blockIdx.x; j < ntl; j += G, it++) {
+  for (uint64_t j = bid; j < ntl; j += G, it++) {
     const uint64_t jn = j + G;
     const uint32_t l = lane_();
     // a chunk of nv = os / 8 values, 16 <= nv <= 8,192 (short last chunks,
@@ -374,7 +401,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
     // the next descriptor (and its batch) before anything is stored, so the
     // counted waits below see only the stores issued after the DMA
     auto next_dma = [&]() {
-      if ((it + 1) % 64 == 0 && jn < ntl) bt = batch_load(kp, it + 1, ntl);
+      if ((it + 1) % 64 == 0 && jn < ntl) bt = batch_load(kp, it + 1, ntl, bid);
       nxt = batch_get(bt, (it + 1) % 64, jn);
       nxt_dma = jn < ntl && fits<MODE>(nxt);
       if (nxt_dma) dma(L, nxt);
@@ -439,10 +466,10 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
       if constexpr (MODE == M_RLE) {
         // run starts: thread t owns runs 4t..4t+3 (length 0 past nr), an
         // exclusive workgroup scan of the lengths
-        uint32_t len[4], s4 = 0;
+        uint32_t len[RPT], s4 = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t r = 4 * threadIdx.x + i;
+        for (int i = 0; i < (int)RPT; i++) {
+          const uint32_t r = RPT * threadIdx.x + i;
           uint32_t x = 0;
           if (ok && r < hd.nr) x = c32(C, hd.dst + 10 * r + 8);
           len[i] = ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
@@ -461,13 +488,13 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
         ok = ok && tot == nv;
         uint32_t a = pre + inc - s4;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          L.T.RS[4 * threadIdx.x + i] = a;
+        for (int i = 0; i < (int)RPT; i++) {
+          L.T.RS[RPT * threadIdx.x + i] = a;
           // run-head scatter: the run holding cell 16 g, for every 16-cell
           // group start inside this run (each written once: the runs tile
           // [0, 8192) when tot == NV; empty runs hold none)
           if (ok)
-            for (uint32_t g = (a + 15) >> 4; 16 * g < a + len[i]; g++) L.T.HD[g] = (uint16_t)(4 * threadIdx.x + i);
+            for (uint32_t g = (a + 15) >> 4; 16 * g < a + len[i]; g++) L.T.HD[g] = (uint16_t)(RPT * threadIdx.x + i);
           a += len[i];
         }
         if (threadIdx.x == NT - 1) L.T.RS[RUNCAP] = a;
@@ -549,7 +576,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
             }
           }
           lds_barrier();  // the round's (wave) totals; in round 1 also: C is free
-          if (h == 1) next_dma();
+          if (h == NR - 1) next_dma();
           if (ok) {
             // start state of the (round, wave) block: 1,024 codes per block
             uint64_t X = 0, D = 0;
@@ -610,7 +637,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
               }
             }
           }
-          if (h == 1) {
+          if (h == NR - 1) {
             lds_barrier();  // every wave is done with C
             next_dma();
           }
@@ -675,7 +702,7 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = base + d[k];
           }
-          if (h == 1) {
+          if (h == NR - 1) {
             lds_barrier();  // every wave is done with C
             next_dma();
           }
@@ -683,12 +710,12 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
         }
       };
       round(std::integral_constant<uint32_t, 0>{});
-      round(std::integral_constant<uint32_t, 1>{});
+      if constexpr (NR == 2) round(std::integral_constant<uint32_t, 1>{});
     }  // cur_dma
     // a tile this kernel does not take goes to the fused kernel
     if (!ok) dmask |= 1ull << (it % 64);
     if ((it + 1) % 64 == 0 || jn >= ntl) {
-      if (dmask && w == 0) queue_batch(kp, dmask, it - it % 64);
+      if (dmask && w == 0) queue_batch(kp, dmask, it - it % 64, bid);
       dmask = 0;
     }
     if (!issued) next_dma();
@@ -701,30 +728,35 @@ __global__ void __launch_bounds__(NT, Occ<MODE>::v) unfilter_stream_small_kernel
     cur_dma = nxt_dma;
     stored = ok;
   }
-  if (kp.stats && threadIdx.x == 0 && ok_tiles && chunked) {
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
-  } else if (kp.stats && threadIdx.x == 0 && ok_tiles) {
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
+  // (one slot of counters per 64 workgroups, summed by the host: a
+  // 100,000-workgroup launch on one address would serialise its atomics)
+  uint64_t* const sl = kp.stats ? kp.stats + TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63)) : nullptr;
+  if (sl && threadIdx.x == 0 && ok_tiles && chunked) {
+    atomicAdd((unsigned long long*)&sl[TDBG_STAT_STREAM_CHUNKS], (unsigned long long)ok_tiles);
+  } else if (sl && threadIdx.x == 0 && ok_tiles) {
+    atomicAdd((unsigned long long*)&sl[TDBG_STAT_FUSED_TILES], (unsigned long long)ok_tiles);
+    atomicAdd((unsigned long long*)&sl[TDBG_STAT_FUSED_BYTES], (unsigned long long)ok_bytes);
+    atomicAdd((unsigned long long*)&sl[TDBG_STAT_STREAM_TILES], (unsigned long long)ok_tiles);
   }
 }
 
-}  // namespace ssm
+}  // namespace TDBG_SSM_NS
 }  // namespace tdbg
 
 // mode: 0 DD (8-byte), 1 RLE (cell size 8), 2 PD + BWR (8-byte); sgn: the
 // BWR stage's integer type is signed
-extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode) {
-  using namespace tdbg::ssm;
+extern "C" uint32_t TDBG_SSM_SYM(tdbg_stream_small_grid)(int cus, int mode) {
+  using namespace tdbg::TDBG_SSM_NS;
   static const int g = tdbg_hook("TDBG_SMALL_GRID") ? atoi(tdbg_hook("TDBG_SMALL_GRID")) : 0;  // experiments
   const int occ = mode == M_DD ? Occ<M_DD>::v : mode == M_RLE ? Occ<M_RLE>::v : Occ<M_PDBWR>::v;
   return g > 0 ? (uint32_t)g : (uint32_t)(cus * occ);
 }
 
-extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
-                                               hipStream_t s) {
-  using namespace tdbg::ssm;
+// (512: grid = the items rounded up to 8, at most 2^22 -- workgroups then loop)
+extern "C" hipError_t TDBG_SSM_SYM(tdbg_launch_stream_small)(const tdbg::KParams* kp, uint32_t grid, int mode,
+                                                             int sgn, hipStream_t s) {
+  using namespace tdbg::TDBG_SSM_NS;
+  if (NP) grid = 8 * ((std::min<uint64_t>(std::max<uint64_t>(kp->ntiles, 1), 1ull << 22) + 7) / 8);
   if (mode == M_DD) {
     TDBG_LAUNCH((unfilter_stream_small_kernel<M_DD, false>), dim3(grid), dim3(NT), s, *kp);
   } else if (mode == M_RLE) {
