@@ -288,13 +288,18 @@ unfilter_c2tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
     const uint32_t rb = S + 8192 * w + 4 * l;
     // row r's dword of lane l.  C2i: decoded from its BWR window on the way
     // (a 256-B row is one window or part of one: a wave-uniform decoder)
+    // (lane q < 32 holds row q's window entry; each row takes it by readlane)
+    uint2 tq = make_uint2(0, 0);
+    if (MODE == 1 && !MAT) {
+      const uint32_t Wq = (8192 * w + 256 * (l & 31)) >> wsh;
+      tq = L.TAB[Wq < wlast ? Wq : wlast];
+    }
     auto row = [&](uint32_t r) -> uint32_t {
       if (MODE == 0 || MAT) return (S & 3) == 0 ? L.IMG[(rb + r * 256) >> 2] : rd32(L.IMG, rb + r * 256);
       const uint32_t o = 8192 * w + 256 * r;
       uint32_t W = o >> wsh;
       W = W < wlast ? W : wlast;
-      const uint2 tv = L.TAB[W];
-      const uint32_t tx = __builtin_amdgcn_readfirstlane(tv.x), mn = __builtin_amdgcn_readfirstlane(tv.y);
+      const uint32_t tx = __builtin_amdgcn_readlane(tq.x, r), mn = __builtin_amdgcn_readlane(tq.y, r);
       const uint32_t kind = tx >> 20;  // (scalar: the row's decoder is a wave-uniform branch)
       const uint32_t x = rd32(L.IMG, (tx & OFFM) + b + (((o - (W << wsh)) >> 2) << kind) + (l << kind));
       return kind == 2 ? x : ext<SGN>(x, 0, 8u << kind) + mn;
