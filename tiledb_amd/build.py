@@ -38,6 +38,7 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           ("tdbg_c2tile.hip", "tdbg_c2tile", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small_512", ["-DTDBG_SMALL_NT=512"]),
+          ("tdbg_stream_small.hip", "tdbg_stream_small_256np", ["-DTDBG_SMALL_NP=1"]),
           ("tdbg_forward_stream.hip", "tdbg_forward_stream", []),
           ("tdbg_forward_small.hip", "tdbg_forward_small", []),
           ("tdbg_forward_shuffle.hip", "tdbg_forward_shuffle", []),

@@ -72,6 +72,8 @@ extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t
                                                hipStream_t s);
 extern "C" hipError_t tdbg_launch_stream_small_512(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                   hipStream_t s);
+extern "C" hipError_t tdbg_launch_stream_small_256np(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
+                                                    hipStream_t s);
 extern "C" uint32_t tdbg_stream_small_grid(int cus, int mode);
 extern "C" hipError_t tdbg_launch_stream_shuffle4(const tdbg::KParams* kp, hipStream_t s);
 extern "C" hipError_t tdbg_launch_dense_frag_copy(const tdbg_dense_frag_config* fc, uint64_t ntiles,
@@ -855,13 +857,17 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("bitshuffle tile kernel launch: ") + hipGetErrorString(e));
     } else if (small_mode >= 0) {
       const int sgn = (small_mode == 2 && P.s[1].sgn) ? 1 : 0;
-      // one 512-thread workgroup per tile (C3a 0.59 -> 0.65-0.69, C3b 0.53 ->
-      // 0.69, C4 0.69 -> 0.75-0.77 of 8 TB/s, profiles/r05/small_np_ab.txt), or
-      // (A/B) the persistent 256-thread kernel, which chunk-parallel launches keep
-      static const bool small_p = tdbg_hook("TDBG_SMALL_P") != nullptr;  // experiments
+      // One workgroup per tile: 256 threads for DD and PD + BWR (C3a 0.59 ->
+      // 0.70-0.72, C4 0.69 -> 0.81), 512 for RLE (C3b 0.53 -> 0.68-0.70;
+      // profiles/r05/small_np_ab.txt).  The persistent 256-thread kernel stays
+      // for chunk-parallel launches (and A/B).
+      static const bool small_p = tdbg_hook("TDBG_SMALL_P") != nullptr;                  // experiments
+      static const long small_nt = tdbg_hook_int("TDBG_SMALL_NT", 0);                    // experiments: 256 / 512
+      const bool w512 = small_nt ? small_nt == 512 : small_mode == 1;
       if (!skip_fused)
         e = small_p ? tdbg_launch_stream_small(&ks, tdbg_stream_small_grid(c->cus, small_mode), small_mode, sgn, stream)
-                    : tdbg_launch_stream_small_512(&ks, 0, small_mode, sgn, stream);
+            : w512  ? tdbg_launch_stream_small_512(&ks, 0, small_mode, sgn, stream)
+                    : tdbg_launch_stream_small_256np(&ks, 0, small_mode, sgn, stream);
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
     } else {
       const int sgn = p->plan.s[2].sgn ? 1 : 0;

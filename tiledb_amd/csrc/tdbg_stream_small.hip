@@ -60,12 +60,20 @@
 // kernel, two rounds of 4,096 values per tile, 4-5 workgroups per CU -- and
 // 512 -- one workgroup per tile (non-persistent, the launch's workgroups
 // dealt XCD-contiguously as in tdbg_c5tile.hip), one round of 8,192 values.
+// (TDBG_SMALL_NP=1 with 256 threads: one tile per workgroup, two rounds;
+// an A/B build)
 #ifndef TDBG_SMALL_NT
 #define TDBG_SMALL_NT 256
 #endif
-#if TDBG_SMALL_NT == 256
+#ifndef TDBG_SMALL_NP
+#define TDBG_SMALL_NP (TDBG_SMALL_NT == 512)
+#endif
+#if TDBG_SMALL_NT == 256 && !TDBG_SMALL_NP
 #define TDBG_SSM_NS ssm
 #define TDBG_SSM_SYM(x) x
+#elif TDBG_SMALL_NT == 256
+#define TDBG_SSM_NS ssm256np
+#define TDBG_SSM_SYM(x) x##_256np
 #elif TDBG_SMALL_NT == 512
 #define TDBG_SSM_NS ssm512
 #define TDBG_SSM_SYM(x) x##_512
@@ -80,7 +88,7 @@ using namespace sc;
 
 constexpr int NT = TDBG_SMALL_NT;
 constexpr int NWV = NT / 64;      // waves per workgroup
-constexpr bool NP = NT == 512;    // one tile per workgroup, XCD-contiguous deal
+constexpr bool NP = TDBG_SMALL_NP;  // one tile per workgroup, XCD-contiguous deal
 constexpr uint32_t NR = 8 / NWV;  // rounds of 1,024 NWV values per tile
 constexpr uint32_t OUTB = 65536;   // output bytes per tile
 constexpr uint32_t NV = OUTB / 8;  // 8-byte values per tile
@@ -327,7 +335,7 @@ __device__ __forceinline__ uint64_t bwr_ext(uint64_t x, uint32_t kind) {
 // DD / RLE then spill)
 template <int MODE>
 struct Occ {
-  static constexpr int v = NP ? 2 : (MODE == M_DD ? 5 : MODE == M_RLE ? 5 : 4);
+  static constexpr int v = NT == 512 ? 2 : (MODE == M_DD ? 5 : MODE == M_RLE ? 5 : 4);
 };
 
 // Queue the declined tiles of one batch (bit i of mask: the workgroup's tile
