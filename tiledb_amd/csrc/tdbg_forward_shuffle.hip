@@ -137,7 +137,13 @@ __global__ void __launch_bounds__(NT, 2) filter_shuffle4_kernel(const KParams kp
   __shared__ uint32_t wsz[NWV];  // C2i: compressed bytes of each wave's 32 windows
   __shared__ uint32_t red[MODE == 2 ? NWV : 1][8][64];  // C2i: a wave's 8 rows being reduced
   uint64_t taken = 0;
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
+  // A grid of at least one workgroup per tile (a multiple of 8): one tile per
+  // workgroup, dealt so that each XCD (workgroups go round-robin over the 8)
+  // takes a contiguous eighth of the tiles; a smaller grid walks the tiles.
+  const uint32_t G = gridDim.x;
+  const bool np = G >= kp.ntiles && (G & 7) == 0;
+  const uint32_t bid = np ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  for (uint64_t j = bid; j < kp.ntiles; j += G) {
     uint32_t T = threadIdx.x;
     asm volatile("" : "+v"(T));
     const uint32_t l = T & 63, w = __builtin_amdgcn_readfirstlane(T >> 6);
@@ -345,7 +351,8 @@ __global__ void __launch_bounds__(NT, 2) filter_shuffle4_kernel(const KParams kp
     }
   }
   if (kp.stats && threadIdx.x == 0 && taken)
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FWD_STREAM_TILES], (unsigned long long)taken);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63)) + TDBG_STAT_FWD_STREAM_TILES],
+              (unsigned long long)taken);  // (one slot per 64 workgroups: tdbg_host.cpp read_stats sums them)
 }
 
 }  // namespace fsh

@@ -227,7 +227,13 @@ template <int MODE, bool SGN>
 __global__ void __launch_bounds__(NT, MODE == 2 ? 3 : 4) filter_small_kernel(const KParams kp) {
   __shared__ Lds L;
   uint64_t taken = 0;
-  for (uint64_t j = blockIdx.x; j < kp.ntiles; j += gridDim.x) {
+  // A grid of at least one workgroup per tile (a multiple of 8): one tile per
+  // workgroup, dealt so that each XCD (workgroups go round-robin over the 8)
+  // takes a contiguous eighth of the tiles; a smaller grid walks the tiles.
+  const uint32_t G = gridDim.x;
+  const bool np = G >= kp.ntiles && (G & 7) == 0;
+  const uint32_t bid = np ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  for (uint64_t j = bid; j < kp.ntiles; j += G) {
     // thread index opaque to the optimizer (per-thread index math is
     // tile-invariant; hoisting it pins registers)
     uint32_t T = threadIdx.x;
@@ -508,7 +514,8 @@ __global__ void __launch_bounds__(NT, MODE == 2 ? 3 : 4) filter_small_kernel(con
     }
   }
   if (kp.stats && threadIdx.x == 0 && taken)
-    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_FWD_STREAM_TILES], (unsigned long long)taken);
+    atomicAdd((unsigned long long*)&kp.stats[TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63)) + TDBG_STAT_FWD_STREAM_TILES],
+              (unsigned long long)taken);  // (one slot per 64 workgroups: tdbg_host.cpp read_stats sums them)
 }
 
 }  // namespace fsm

@@ -1169,6 +1169,12 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
                        P.s[1].w == 4 && P.s[1].dts == 4 && P.s[1].window == 256)
                         ? 2
                         : -1;
+  // The shuffle and small forward kernels: one workgroup per tile (a grid of
+  // the tiles rounded up to 8, XCD-contiguous) up to 2^22 tiles, else (and
+  // for A/B) a persistent grid walking the tiles
+  static const bool fwd_p = tdbg_hook("TDBG_FWD_P") != nullptr;  // experiments
+  const bool fwd_np = !fwd_p && n <= (1ull << 22);
+  const uint32_t np_grid = (uint32_t)(8 * ((std::max<uint64_t>(n, 1) + 7) / 8));
   hipError_t e = hipSuccess;
   if (fshuf >= 0) {
     HIP_OK(hipMemsetAsync(c->d_fbq, 0, sizeof(uint32_t), s));
@@ -1176,7 +1182,8 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kf.fbq = c->d_fbq;
     kf.fbq_cap = (uint32_t)n;
     kf.stats = c->d_stats;
-    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
+    // (C2i, BWR active: the persistent grid measured 1.5 % faster)
+    const uint32_t fgrid = fwd_np && fshuf != 2 ? np_grid : (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * 2);
     e = tdbg_launch_filter_shuffle4(&kf, fgrid, fshuf, fshuf == 2 && P.s[1].sgn ? 1 : 0, s);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward shuffle launch: ") + hipGetErrorString(e));
     kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
@@ -1188,7 +1195,7 @@ static int filter_launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t n, co
     kf.fbq = c->d_fbq;
     kf.fbq_cap = (uint32_t)n;
     kf.stats = c->d_stats;
-    const uint32_t fgrid = (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * (fsmall == 2 ? 3 : 4));
+    const uint32_t fgrid = fwd_np ? np_grid : (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus * (fsmall == 2 ? 3 : 4));
     e = tdbg_launch_filter_small(&kf, fgrid, fsmall, fsmall == 0 && P.s[0].sgn ? 1 : 0, s);
     if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("forward small launch: ") + hipGetErrorString(e));
     kp.tile_list = c->d_fbq + 1;  // the general kernel on the queue
