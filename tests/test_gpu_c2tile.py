@@ -74,10 +74,23 @@ def crafted(kinds: str, rng, nbytes: int = 65536, window: int = 256) -> np.ndarr
     return v
 
 
-def _tile_mode(eng, ctx, O, case, align=1):
+def c2_taken(f: np.ndarray, bwr: bool) -> bool:
+    """The C2 tile kernel decodes this tile: one chunk of 256..65,536 bytes
+    (a multiple of 4) and, with BWR, window 0 a power of two in [256, 4096]."""
+    nch = int(np.frombuffer(f[:8].tobytes(), dtype="<u8")[0])
+    orig = int(np.frombuffer(f[8:12].tobytes(), dtype="<u4")[0])
+    if nch != 1 or orig < 256 or orig > 65536 or orig % 4:
+        return False
+    if not bwr:
+        return True
+    ws = int(np.frombuffer(f[20 + 13:20 + 17].tobytes(), dtype="<u4")[0])
+    return 256 <= ws <= 4096 and ws & (ws - 1) == 0
+
+
+def _tile_mode(eng, ctx, O, case, align=1, bwr=None):
     """Tile-mode launch of >= MIN_TILES tiles cycling over the case's tiles:
     bit-exact vs the oracle; returns (n, fused, fallback, taken by the kernel,
-    64 KiB tiles)."""
+    tiles it should take)."""
     from tests.test_gpu_parity import check_parity_replicated, encode
     _, enc = encode(O, case)
     assert len(enc) == len(case.tiles)
@@ -87,7 +100,9 @@ def _tile_mode(eng, ctx, O, case, align=1):
     st = check_parity_replicated(eng, ctx, O, case, enc, n, align=align)
     assert not st.any()
     f1, b1, _ = ctx.path_stats()
-    want = sum(enc[i % len(enc)][2] == 65536 for i in range(n))
+    if bwr is None:
+        bwr = len(case.pipeline.filters) == 2 and int(case.dtype) != int(Datatype.FLOAT32)
+    want = sum(c2_taken(enc[i % len(enc)][0], bwr) for i in range(n))
     return n, f1 - f0, b1 - b0, ctx.stream_tiles() - s0, want
 
 
@@ -127,11 +142,11 @@ def test_c2i_window_kinds(eng, ctx, oracle_mod, dtype, window):
 
 @pytest.mark.parametrize("bwr", [False, True])
 def test_c2_declined_shapes(eng, ctx, oracle_mod, bwr):
-    """Tiles the kernel leaves to the fused kernel in the same launch (not
-    64 KiB: 40,000 B, 65,532 B, 8 B; two chunks: 128 KiB) mixed with ones it
-    takes (outputs back to back: at every 4-B alignment): bit-exact, and it
-    took exactly the one-chunk 64 KiB tiles (the
-    fused kernel passes one of the odd shapes on to the general interpreter)."""
+    """Tiles the kernel leaves to the fused kernel in the same launch (8 B;
+    two chunks: 128 KiB) mixed with ones it takes (64 KiB, 40,000 B, 65,532 B;
+    outputs back to back: at every 4-B alignment): bit-exact, and it took
+    exactly the one-chunk tiles of 256 B or more (the fused kernel passes one
+    of the odd shapes on to the general interpreter)."""
     rng = np.random.default_rng(41 + bwr)
     vals = [crafted("8hr", rng), rng.integers(-2**31, 2**31, 10000).astype(np.int32),
             crafted("r", rng), rng.integers(-5, 5, 16383).astype(np.int32),
@@ -140,4 +155,30 @@ def test_c2_declined_shapes(eng, ctx, oracle_mod, bwr):
     case = Case(f"c2_declined_{bwr}", pipe, Datatype.INT32, 4, [as_u8(v) for v in vals])
     n, fused, fb, st, want = _tile_mode(eng, ctx, oracle_mod, case)
     assert 0 < want < n and fb <= n // 6 + 1
+    assert st == want, f"C2 tile kernel took {st}, expected {want}"
+
+
+# every size class of a one-chunk tile: whole 8,192-B blocks or a partial last
+# block (rows of R < 256 bytes, R % 4 = 0 or 2), os % 8 = 4 (a second,
+# copied bitshuffle part), short tiles down to 256 B
+_SIZES = [256, 260, 1000, 1004, 4100, 8192, 8196, 12288, 12292, 40000, 40004, 40960, 65528, 65532, 65536]
+
+
+@pytest.mark.parametrize("dtype,window", [(Datatype.FLOAT32, 0), (Datatype.INT32, 0), (Datatype.INT32, 256),
+                                          (Datatype.UINT32, 1024)])
+def test_c2_every_size_class(eng, ctx, oracle_mod, dtype, window):
+    """One launch of tiles of every size class back to back (outputs at every
+    4-B alignment), [BITSHUFFLE] or [BITSHUFFLE, BWR(window)]: bit-exact, and
+    the kernel takes exactly the tiles it decodes (BWR: window 0 a power of
+    two >= 256 B, so a tile under the window size is left unless it is one)."""
+    rng = np.random.default_rng(77 + window + int(dtype))
+    vals = []
+    for k, nb in enumerate(_SIZES):
+        v = crafted("8hrnzm"[k % 6] + "8r", rng)[: nb // 4] if window else rng.normal(0, 1e3, nb // 4).astype(np.float32)
+        vals.append(v.view(np.uint32) if dtype == Datatype.UINT32 else v.view(np.int32) if dtype == Datatype.INT32 else v)
+    pipe = P(BitshuffleFilter(), BitWidthReductionFilter(window)) if window else P(BitshuffleFilter())
+    case = Case(f"c2_sizes_{int(dtype)}_{window}", pipe, dtype, 4, [as_u8(v) for v in vals])
+    n, fused, fb, st, want = _tile_mode(eng, ctx, oracle_mod, case, bwr=bool(window))
+    assert want >= n // 2, want
+    assert fb <= n - want  # (the fused kernel may pass a declined odd shape on to the general interpreter)
     assert st == want, f"C2 tile kernel took {st}, expected {want}"
