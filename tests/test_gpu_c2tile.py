@@ -182,3 +182,44 @@ def test_c2_every_size_class(eng, ctx, oracle_mod, dtype, window):
     assert want >= n // 2, want
     assert fb <= n - want  # (the fused kernel may pass a declined odd shape on to the general interpreter)
     assert st == want, f"C2 tile kernel took {st}, expected {want}"
+
+
+@pytest.mark.parametrize("bwr", [False, True])
+def test_c2_malformed_tiles(eng, ctx, oracle_mod, bwr):
+    """Valid 64 KiB tiles with one header or metadata field corrupted (chunk
+    count, orig, bitshuffle part count / size, BWR window bytes / bits, a
+    truncated image): the tile kernel declines each, and the statuses and
+    bytes of the whole launch equal the oracle's."""
+    import struct
+    from tests.test_gpu_parity import check_parity_replicated
+    rng = np.random.default_rng(91 + bwr)
+    pipe = P(BitshuffleFilter(), BitWidthReductionFilter(256)) if bwr else P(BitshuffleFilter())
+    dtype = Datatype.INT32
+    op = oracle_mod.OraclePipeline(pipe.serialize(), 23, int(dtype), 4)
+    good = [np.frombuffer(op.filter_tile(as_u8(crafted("8hr", rng))), dtype=np.uint8) for _ in range(3)]
+    bad = []
+    m = 20
+    bmd = m + (8 + 9 * 256 if bwr else 0)  # the bitshuffle md (256 BWR windows of 256 B)
+
+    def patch(t, off, fmt, val):
+        b = bytearray(t.tobytes())
+        struct.pack_into(fmt, b, off, val)
+        return np.frombuffer(bytes(b), dtype=np.uint8)
+
+    bad.append(patch(good[0], 0, "<Q", 2))             # chunk count
+    bad.append(patch(good[0], 8, "<I", 65532))         # orig
+    bad.append(patch(good[1], bmd, "<I", 2))           # bitshuffle parts
+    bad.append(patch(good[1], bmd + 4, "<I", 65528))   # bitshuffle part size
+    if bwr:
+        bad.append(patch(good[2], m + 8 + 5, "<I", 252))   # window 0 bytes
+        bad.append(patch(good[2], m + 8 + 9 * 7 + 4, "<B", 12))  # window 7 bits
+    bad.append(good[2][: len(good[2]) - 100].copy())   # truncated
+    enc = [(t, None, 65536) for t in good + bad]
+    case = Case(f"c2_malformed_{bwr}", pipe, dtype, 4, [])
+    f0, b0, _ = ctx.path_stats()
+    s0 = ctx.stream_tiles()
+    st = check_parity_replicated(eng, ctx, oracle_mod, case, enc, MIN_TILES)
+    taken = ctx.stream_tiles() - s0
+    n_good = sum(1 for i in range(MIN_TILES) if i % len(enc) < len(good))
+    assert taken == n_good, f"C2 tile kernel took {taken}, expected {n_good}"
+    assert (st != 0).sum() > 0
