@@ -329,17 +329,30 @@ def cpu_baseline(engine, dp, packed, offs, sizes, out_bytes, ntiles_sample: int,
 TRAFFIC_FILE = "profiles/pmc_traffic.json"
 
 
-def load_traffic(cfg: str, variant: str):
-    """HBM bytes per launch of the same workload from the committed rocprofv3
-    --pmc FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh): not measured in this
-    run (PMC counters need their own rocprofv3 passes)."""
+def load_traffic(cfg: str, variant: str, b_alg: float | None = None):
+    """(HBM bytes per launch, source) for this launch from the committed
+    rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/profile.sh): not
+    measured in this run (PMC counters need their own rocprofv3 passes).
+
+    A PMC pass is this launch's only when it ran the same workload at the same
+    size: its algorithmic bytes equal `b_alg` (within 0.1 %).  Otherwise (a
+    rank's shard at N > 1, a --tiles-per-gpu run) the pass's measured
+    traffic / B_alg ratio is applied to this launch's B_alg and labelled
+    "scaled"; with no pass of the workload at all, (None, None)."""
     path = os.path.join(ROOT, TRAFFIC_FILE)
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(f"{cfg}_{variant}", {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(f"{cfg}_{variant}", {})
     except Exception:
-        return None
+        return None, None
+    hbm, alg = e.get("hbm_bytes_per_launch"), e.get("algorithmic_bytes_per_launch")
+    if hbm is None:
+        return None, None
+    if b_alg is None or not alg:
+        return (hbm, "measured") if b_alg is None else (None, None)
+    if abs(alg - b_alg) <= 1e-3 * b_alg:
+        return int(hbm), "measured"
+    return int(round(hbm / alg * b_alg)), f"scaled: {hbm / alg:.4f} x B_alg (PMC pass at {alg:.4g} B_alg)"
 
 
 def run_config(engine, ctx, W, args, cfgname, variants, ntiles, steps, warmup, dist, world, rank,
@@ -471,7 +484,7 @@ def kernel_name(cfgname, r):
 
 def roofline(cfgname, var, r):
     achieved = r["b_alg"] / (r["kern_ms"] * 1e-3) / 1e9
-    traffic = load_traffic(cfgname, var)
+    traffic, tsrc = load_traffic(cfgname, var, r["b_alg"])
     return {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -479,7 +492,7 @@ def roofline(cfgname, var, r):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "traffic_source": f"{TRAFFIC_FILE} (committed rocprofv3 --pmc passes of this workload)" if traffic else None,
+        "traffic_source": f"{TRAFFIC_FILE} ({tsrc})" if traffic else None,
         # kernel_ms: the launch's unfilter kernels on its stream, HIP events
         "kernel": kernel_name(cfgname, r),
         "kernel_ms": round(r["kern_ms"], 4),
@@ -498,7 +511,7 @@ def variant_line(cfgname, var, r, world):
             "fallback_tiles_timed": r["fallback"], "stream_tiles_timed": r["streamed"],
             "stream_chunks_timed": r.get("stream_chunks", 0),
             "algorithmic_bytes_per_launch": int(r["b_alg"]),
-            "traffic": load_traffic(cfgname, var)}
+            "traffic": load_traffic(cfgname, var, r["b_alg"])[0]}
 
 
 def cgroup_cpus():
@@ -773,6 +786,59 @@ def dense_var_leg(engine, ctx, steps: int, tiles_side: int = 32, seed: int = 9, 
             "ms_per_call": round(el * 1e3, 3), "GiBps_result": round(res_bytes / el / 2**30, 2)}
 
 
+def compact_line(line: dict, legs_file) -> dict:
+    """The headline JSON the driver parses: the contract's fields, the
+    headline roofline and cpu_baseline, and one GiB/s + roofline fraction per
+    variant and per other leg.  Every leg's detail (kernel names, event
+    times, CPU curves, dense var leg, ...) is in the full line / `legs_file`."""
+    c = line["config"]
+    rf = line["roofline"]
+    out = {k: line[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    tr = lambda v: (round(v["traffic"] / v["algorithmic_bytes_per_launch"], 4)  # noqa: E731
+                    if v.get("traffic") else None)
+    cc = {"workload": c["workload"], "tiles_per_gpu": c["tiles_per_gpu"], "variant": c["variant"],
+          "parallelism": c["parallelism"], "fallback_tiles_timed": c["fallback_tiles_timed"],
+          "variants": {v: {"GiBps": x["GiBps"], "roofline_frac": x["roofline_frac"], "kernel_ms": x["kernel_ms"],
+                           "ms_per_step": x["ms_per_step"], "traffic_over_alg": tr(x)}
+                       for v, x in c["variants"].items()},
+          "min_over_variants_roofline_frac": c["min_over_variants_roofline_frac"]}
+    if "forward" in line:
+        f = line["forward"]
+        cc["forward"] = {"GiBps": f.get("value"), "roofline_frac": f.get("roofline_frac"), "tiles": f.get("tiles_per_gpu")}
+    if "e2e_GiBps" in c:
+        cc["e2e_GiBps_pcie_inclusive"] = c["e2e_GiBps"]
+    if "other_configs" in c:
+        oc = {}
+        for k, o in c["other_configs"].items():
+            e = {"GiBps": o["value_GiBps"], "roofline_frac": o["roofline"]["frac"],
+                 "traffic_over_alg": (round(o["roofline"]["traffic"] / o["roofline"]["algorithmic_bytes_per_launch"], 4)
+                                      if o["roofline"].get("traffic") else None)}
+            if isinstance(o.get("forward"), dict) and "roofline_frac" in o["forward"]:
+                e["forward_frac"] = o["forward"]["roofline_frac"]
+            if "cpu_baseline" in o:
+                e["cpu_GiBps"] = o["cpu_baseline"]["value"]
+            oc[k] = e
+        cc["other_configs"] = oc
+    if "c3_combined" in c:
+        cc["c3_combined"] = {k: c["c3_combined"][k] for k in ("GiBps", "roofline_frac")}
+    for leg in ("c5_shard_12500", "c5_40000B_tiles", "c5_4MiB_tiles"):
+        if leg in c:
+            cc[leg] = {v: {"GiBps": x["GiBps"], "roofline_frac": x["roofline_frac"],
+                           "ms_per_step": x["ms_per_step"], "kernel_ms": x["kernel_ms"]}
+                       for v, x in c[leg]["variants"].items()}
+    cc["legs_file"] = legs_file or "(the line before this one)"
+    out["config"] = cc
+    out["roofline"] = {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+                                           "kernel", "kernel_ms", "algorithmic_bytes_per_launch")}
+    if "cpu_baseline" in line:
+        cb = line["cpu_baseline"]
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+        if "per_thread_GiBps" in cb:
+            out["cpu_baseline"]["per_thread_GiBps"] = cb["per_thread_GiBps"]
+    return out
+
+
 def init_dist(dist_mod, torch, env, local: int) -> str:
     """One process per GPU: RCCL ('nccl') bound to the rank's own device
     (init_process_group(device_id=cuda:local)), or the gloo rehearsal
@@ -825,6 +891,8 @@ def main():
                     help="N = 1 run: also time C5 on one GPU's shard of an 8-GPU node (100k / 8)")
     ap.add_argument("--c5s-tiles", type=int, default=CONFIGS["c5s"]["tiles_per_gpu"],
                     help="N = 1 run: also time the C5 pipeline on 40,000-B tiles (0 = skip)")
+    ap.add_argument("--legs-file", default="gpurun_out/bench_legs.json",
+                    help="every leg's full JSON (also printed on the line before the headline); '' = none")
     args = ap.parse_args()
 
     import torch
@@ -928,7 +996,19 @@ def main():
         # same job over more GPUs; the CPU figure does not change with N)
         line["cpu_baseline"] = cpu_line(engine, dp, r, args.config, head, threads, args.cpu_seconds, scaling=True)
     if rank == 0:
-        print(json.dumps(line))
+        # every leg in full: a side file and an earlier stdout line; the last
+        # line is the compact headline the driver parses (<= ~4 KB)
+        full = json.dumps(line)
+        legs = args.legs_file
+        if legs:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(legs)), exist_ok=True)
+                with open(legs, "w") as fh:
+                    fh.write(full + "\n")
+            except OSError:
+                legs = None
+        print(full)
+        print(json.dumps(compact_line(line, legs)))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -500,7 +500,9 @@ int tdbg_dense_copy_fragments_async(tdbg_context* ctx, const tdbg_dense_frag_con
  * (*d_var_total, device); the cells' source addresses stay in ctx for step 2.
  * A cell whose offsets o[i] <= o[i + 1] <= o[tile cells] do not hold is
  * read as empty (nothing is read outside a var tile) and flags the context;
- * tdbg_dense_read_var_host returns TDBG_E_DATA_READ for it. */
+ * the flag is cleared on `stream` at the start of every call, and
+ * tdbg_dense_var_status reports it (tdbg_dense_read_var_host returns
+ * TDBG_E_DATA_READ for it). */
 int tdbg_dense_var_offsets_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg, uint64_t ntiles,
                                  const int64_t* d_tile_start, const int64_t* d_frag_dom,
                                  const uint8_t* const* d_offset_tiles, const uint8_t* const* d_var_tiles,
@@ -512,6 +514,12 @@ int tdbg_dense_var_offsets_async(tdbg_context* ctx, const tdbg_dense_frag_config
 int tdbg_dense_var_copy_async(tdbg_context* ctx, const tdbg_dense_frag_config* cfg,
                               const uint64_t* d_result_offsets, const uint64_t* d_var_total, uint8_t* d_result_var,
                               tdbg_stream stream);
+/* The data check of the last tdbg_dense_var_offsets_async on ctx: waits for
+ * `stream` (the one that call ran on), then *status = TDBG_OK, or
+ * TDBG_E_DATA_READ when a cell's offsets lay outside its var tile (those
+ * cells were read as empty, as the reference's Status_ReaderError for a
+ * corrupt offsets tile fails the read). */
+int tdbg_dense_var_status(tdbg_context* ctx, tdbg_stream stream, int32_t* status);
 
 /* Host-resident var-sized dense read fused with the transfers: the filtered
  * offsets and var tiles of every (space tile, fragment) -> H2D -> unfilter

@@ -11,7 +11,10 @@ def test_source_digest_is_stable_and_covers_every_unit():
     d1, d2 = B.source_digest(), B.source_digest()
     assert d1 == d2 and len(d1) == 64
     srcs = {s for s, _, _ in B.UNITS}
-    assert {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_host.cpp"} <= srcs
+    assert {"tdbg_c5tile.hip", "tdbg_c2tile.hip", "tdbg_host.cpp"} <= srcs
+    # (the retired round-4 streaming kernels are in the experiments library only)
+    assert not {"tdbg_stream.hip", "tdbg_stream_raw.hip"} & srcs
+    assert {"tdbg_stream.hip", "tdbg_stream_raw.hip"} <= {s for s, _, _ in B.EXP_ONLY_UNITS}
     for s in srcs:
         assert os.path.exists(os.path.join(B.CSRC, s))
 
@@ -23,3 +26,14 @@ def test_loaded_library_was_built_from_this_tree():
     pv = B.provenance()
     assert pv["sources_match"], "libtiledb_amd.so was built from other sources: rebuild (build())"
     assert pv["library_match"], "libtiledb_amd.so differs from the one its manifest records"
+
+
+def test_product_library_has_no_retired_kernels():
+    """VERDICT r5 hygiene: round 4's streaming C5 kernels (replaced by the
+    tile kernel) are built into the experiments library only."""
+    if not os.path.exists(B.LIB):
+        pytest.skip("library not built")
+    blob = open(B.LIB, "rb").read()
+    assert b"unfilter_c5tile_kernel" in blob
+    for name in (b"unfilter_stream_raw_kernel", b"unfilter_stream_kernel", b"tdbg_launch_stream_raw"):
+        assert name not in blob, name

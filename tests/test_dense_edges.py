@@ -222,3 +222,57 @@ def test_dense_read_var_host_offsets_outside_var_tile(oracle_mod):
     rc, got_o, got_d, st = engine.dense_read_var_host(ctx, dpo, dpv, fc, starts, np.array(doms, dtype=np.int64),
                                                       off_f, var_f, var_u, b"\x00", 1 << 16)
     assert rc == 0 and np.array_equal(got_o, want_o) and got_d == want_d
+
+
+def test_dense_var_offsets_async_flag_is_per_call(oracle_mod):
+    """the async offsets entry clears the context's data flag on
+    the caller's stream at every call, and tdbg_dense_var_status reports it.
+    Bad offsets -> TDBG_E_DATA_READ from the status query; the next async call
+    with good offsets -> TDBG_OK; a host read on the same context then
+    matches the oracle (the flag no longer outlives its call)."""
+    import torch
+    from tiledb_amd import engine
+    rng = np.random.default_rng(29)
+    ext, lo, hi = (4, 8), (0, 0), (3, 15)
+    starts = np.array([(0, 0), (0, 8)], dtype=np.int64)
+    doms = [[(0, 3), (0, 15)]]
+    fc = engine.dense_frag_config(8, ext, lo, hi, 1, 1, 0, 0)
+    keep = []
+    ctx = engine.Context(0)
+
+    def run(bad):
+        offs_t, var_t, want_tot = [], [], 0
+        for t in range(2):
+            _, o_x, var = _var_tiles(rng, 32, 5)
+            if bad and t == 1:
+                o_x[20] = var.size + 40  # past the var tile's end
+            want_tot += var.size
+            offs_t.append(_dev(o_x.view(np.int64), keep))
+            var_t.append(_dev(var if var.size else np.zeros(1, np.uint8), keep))
+        d_off = torch.zeros(64, dtype=torch.int64, device="cuda:0")
+        d_tot = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+        d_fill = _dev(np.zeros(1, np.uint8), keep)
+        engine.dense_var_offsets_async(ctx, fc, 2, _dev(starts.reshape(-1), keep),
+                                       _dev(np.array(doms, dtype=np.int64).reshape(-1), keep),
+                                       _ptr_table(offs_t, keep), _ptr_table(var_t, keep), d_fill,
+                                       d_off.data_ptr(), d_tot.data_ptr())
+        return engine.dense_var_status(ctx), int(d_tot.item()), want_tot
+
+    st, _, _ = run(True)
+    assert st == 5  # TDBG_E_DATA_READ
+    st, tot, want = run(False)
+    assert st == 0 and tot == want
+    st, _, _ = run(True)
+    assert st == 5
+    # a good host read on the same context right after a flagged async call
+    nfrag, present = 1, [[True], [True]]
+    offp = FilterPipeline(65536, [PositiveDeltaFilter(1024), BitWidthReductionFilter(256)])
+    varp = FilterPipeline(65536, [BitWidthReductionFilter(256)])
+    off_f, var_f, var_u, off_unf, var_unf = _var_inputs(oracle_mod, rng, starts, ext, nfrag, present, offp, varp,
+                                                        Datatype.UINT8, 5)
+    want_o, want_d = oracle_mod.dense_var_read(off_unf, var_unf, starts, ext, lo, hi, doms, b"\x00", 0, 0)
+    dpo = engine.DevicePipeline(offp.serialize(), 23, int(Datatype.UINT64), 8)
+    dpv = engine.DevicePipeline(varp.serialize(), 23, int(Datatype.UINT8), 1)
+    rc, got_o, got_d, st = engine.dense_read_var_host(ctx, dpo, dpv, fc, starts, np.array(doms, dtype=np.int64),
+                                                      off_f, var_f, var_u, b"\x00", 1 << 16)
+    assert rc == 0 and np.array_equal(got_o, want_o) and got_d == want_d

@@ -121,6 +121,20 @@ def test_two_rank_shards_cover_every_tile_once():
     assert abs(line["value"] - job / (line["ms_per_step"] * 1e-3) / 2**30) < 1e-3 * line["value"] + 0.01
     assert line["roofline"]["bound"] == "hbm" and 0 < line["roofline"]["frac"]
     assert "cpu_baseline" not in line
+    # the rank's HBM traffic is its own shard's (the 100k-tile PMC pass's
+    # traffic / B_alg ratio applied to this rank's B_alg), not the 100k figure
+    rf = line["roofline"]
+    assert rf["traffic"] and 0.99 < rf["traffic"] / rf["algorithmic_bytes_per_launch"] < 1.05
+    assert "scaled" in rf["traffic_source"]
+    # the last stdout line the driver parses stays compact
+    import json
+    import bench
+    c = bench.compact_line(line, None)
+    assert len(json.dumps(c)) < 6000
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "roofline"):
+        assert k in c
+    assert c["config"]["workload"] and c["config"]["tiles_per_gpu"] == line["config"]["tiles_per_gpu"]
+    assert c["roofline"]["traffic"] == rf["traffic"]
     assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0 and cb["unit"] == "GiB/s"
 
 

@@ -1,12 +1,15 @@
-"""GPU parity of the streaming kernels for the headline pipeline
-[BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)] on INT32 / UINT32
-(tiledb_amd/csrc/tdbg_stream.hip for bit-packed DoubleDelta,
-tdbg_stream_raw.hip for DoubleDelta stored raw), through the C-ABI.
+"""GPU parity of the C5 tile kernel (tiledb_amd/csrc/tdbg_c5tile.hip,
+unfilter_c5tile_kernel: one workgroup per tile) for the headline pipeline
+[BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION(256)] on INT32 / UINT32,
+DoubleDelta bit-packed (the coded path) and stored raw (the raw path),
+through the C-ABI.  (These tests exercised round 4's streaming kernels,
+tdbg_stream.hip / tdbg_stream_raw.hip, before the tile kernel replaced them;
+those now live in the experiments library only.)
 
-Bit-exact against the oracle, with the streaming kernels proven to have taken
-the tiles they are built for (tdbg_context_stream_stats /
-tdbg_context_stream_raw_stats), every DD code width cb = 2..31 and every
-raw-kernel window decoder (all-raw, all-8-bit, mixed/16-bit) exercised;
+Bit-exact against the oracle, with the tile kernel proven to have taken the
+tiles it is built for (tdbg_context_stream_stats: coded + raw tiles;
+tdbg_context_stream_raw_stats: raw tiles), every DD code width cb = 2..31 and
+every raw-path window decoder (all-raw, all-8-bit, mixed/16-bit) exercised;
 tiles they decline (odd shapes, corrupted) must come out exactly as the
 oracle says through the fused kernel and the general interpreter behind it.
 """
@@ -21,7 +24,7 @@ from tiledb_amd.filter_pipeline import BitWidthReductionFilter, ByteshuffleFilte
 
 pytestmark = pytest.mark.gpu
 
-CCAP = 22016  # tdbg_stream.hip: tile image bytes staged in LDS
+CCAP = 22016  # (round 4's coded-kernel image cap: tiles on both sides of it are tested)
 
 
 @pytest.fixture(scope="module")
@@ -118,7 +121,7 @@ def raw_window_values(kinds, rng) -> np.ndarray:
 
 
 @pytest.mark.parametrize("align", [1, 16])
-def test_stream_active_tiles(eng, ctx, oracle_mod, align):
+def test_c5tile_coded_active_tiles(eng, ctx, oracle_mod, align):
     """C5 'active' tiles: every one taken by the streaming kernel."""
     pool, vals = W.c5_pool("active", 24, seed=21)
     case = Case("c5_active", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
@@ -127,7 +130,7 @@ def test_stream_active_tiles(eng, ctx, oracle_mod, align):
     assert st == len(enc), f"streaming kernel took {st} of {len(enc)} tiles"
 
 
-def test_stream_every_code_width(eng, ctx, oracle_mod):
+def test_c5tile_coded_every_code_width(eng, ctx, oracle_mod):
     """DD bitsize 1..30 (code widths 2..31, every instantiation), two tiles each."""
     rng = np.random.default_rng(22)
     vals = [step_values(b, rng) for b in range(1, 31) for _ in range(2)]
@@ -141,7 +144,7 @@ def test_stream_every_code_width(eng, ctx, oracle_mod):
     assert st == want, f"streaming kernel took {st}, expected {want}"
 
 
-def test_stream_uint32(eng, ctx, oracle_mod):
+def test_c5tile_coded_uint32(eng, ctx, oracle_mod):
     """UINT32 (BWR zero-extends its 8/16-bit windows: spec 20)."""
     rng = np.random.default_rng(23)
     vals = [step_values(b, rng).view(np.uint32) for b in (3, 9, 17, 28)]
@@ -152,7 +155,7 @@ def test_stream_uint32(eng, ctx, oracle_mod):
     assert st >= len(enc) - 2 * (len(enc) // len(vals))
 
 
-def test_stream_mixed_and_declined(eng, ctx, oracle_mod):
+def test_c5tile_coded_mixed_and_declined(eng, ctx, oracle_mod):
     """Active, ramp (DD raw), rand (DD and BWR raw) and step tiles interleaved
     back to back: each streaming kernel takes exactly its eligible tiles, the
     fused kernel the rest, all bit-exact."""
@@ -182,7 +185,7 @@ def _run_raw(eng, ctx, O, case, align=1):
 
 @pytest.mark.parametrize("variant", ["rand", "ramp"])
 @pytest.mark.parametrize("align", [1, 16])
-def test_stream_raw_tiles(eng, ctx, oracle_mod, variant, align):
+def test_c5tile_raw_tiles(eng, ctx, oracle_mod, variant, align):
     """SURVEY's C5 'rand' (DD and BWR raw) and 'ramp' (DD raw, raw and 8-bit
     windows) tiles: every one taken by the raw-DD streaming kernel."""
     pool, vals = W.c5_pool(variant, 16, seed=31)
@@ -195,7 +198,7 @@ def test_stream_raw_tiles(eng, ctx, oracle_mod, variant, align):
 
 @pytest.mark.parametrize("kinds", [(8, 8, 8, 32), (16, 32), (8, 16, 32), (32, 8), (16, 16, 16, 8, 32)],
                          ids=lambda k: "w" + "_".join(map(str, k)))
-def test_stream_raw_window_decoders(eng, ctx, oracle_mod, kinds):
+def test_c5tile_raw_window_decoders(eng, ctx, oracle_mod, kinds):
     """Raw-DD tiles whose BWR windows are 8-bit, 16-bit and raw in runs:
     job planes over all-raw, all-8-bit and mixed / 16-bit windows (the raw
     kernel's three decoders), including window-boundary minimum changes."""
@@ -209,7 +212,7 @@ def test_stream_raw_window_decoders(eng, ctx, oracle_mod, kinds):
     assert fb == 0 and fused == len(enc) and raw == want
 
 
-def test_stream_raw_uint32(eng, ctx, oracle_mod):
+def test_c5tile_raw_uint32(eng, ctx, oracle_mod):
     """UINT32: the raw kernel zero-extends 8/16-bit windows."""
     rng = np.random.default_rng(33)
     vals = [raw_window_values((8, 16, 32), rng).view(np.uint32) for _ in range(4)]
@@ -220,7 +223,7 @@ def test_stream_raw_uint32(eng, ctx, oracle_mod):
 
 
 @pytest.mark.parametrize("window", [512, 1024, 4096, 128, 384])
-def test_stream_raw_window_sizes(eng, ctx, oracle_mod, window):
+def test_c5tile_raw_window_sizes(eng, ctx, oracle_mod, window):
     """BWR windows of 512..4096 B are taken; 128 B (513 windows > 320) and a
     window that is not a power of two (384) are declined to the fused kernel."""
     rng = np.random.default_rng(window)
@@ -234,7 +237,7 @@ def test_stream_raw_window_sizes(eng, ctx, oracle_mod, window):
     assert raw == (len(enc) if taken else 0)  # (declined ones: parity checked, any path)
 
 
-def test_stream_raw_corrupted_tiles(eng, ctx, oracle_mod):
+def test_c5tile_raw_corrupted_tiles(eng, ctx, oracle_mod):
     """Corruptions of raw-DD tiles (tile and chunk headers, BWR metadata,
     compression frame, both DD headers, data, truncation) get the oracle's
     status and bytes; intact tiles beside them are taken by the raw kernel."""
@@ -263,7 +266,7 @@ def test_stream_raw_corrupted_tiles(eng, ctx, oracle_mod):
     assert ctx.stream_raw_tiles() > r0
 
 
-def test_stream_raw_wrong_sizes_and_offsets(eng, ctx, oracle_mod):
+def test_c5tile_raw_wrong_sizes_and_offsets(eng, ctx, oracle_mod):
     """Raw-DD tiles with a wrong output size, and as offsets tiles, are
     declined by the raw kernel and get the oracle's status."""
     from tests.test_gpu_parity import check_parity
@@ -275,7 +278,7 @@ def test_stream_raw_wrong_sizes_and_offsets(eng, ctx, oracle_mod):
     check_parity(eng, ctx, oracle_mod, case, tiles, sizes)
 
 
-def test_stream_corrupted_tiles(eng, ctx, oracle_mod):
+def test_c5tile_coded_corrupted_tiles(eng, ctx, oracle_mod):
     """Corruptions of active tiles (headers, metadata, DD header, truncation)
     get the oracle's status; untouched tiles beside them stay exact."""
     from tests.test_gpu_parity import check_parity

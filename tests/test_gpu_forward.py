@@ -270,7 +270,7 @@ def test_forward_stream_c5_kernel(eng, ctx, oracle_mod):
     (tdbg_context_forward_stream_stats)."""
     import workloads as W
     from tests.cases import c5_tiles, P, DD, Case
-    from tests.test_gpu_stream import step_values
+    from tests.test_gpu_c5tile import step_values
     from tiledb_amd.filter_pipeline import ByteshuffleFilter, BitWidthReductionFilter, Datatype
     rng = np.random.default_rng(61)
     vals = [step_values(b, rng) for b in range(1, 33)]

@@ -106,6 +106,7 @@ SIGNATURES = {
     "tdbg_dense_var_offsets_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                     c_vp, c_vp, c_vp, c_vp]),
     "tdbg_dense_var_copy_async": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "tdbg_dense_var_status": (ctypes.c_int, [c_vp, c_vp, c_i32p]),
     "tdbg_dense_read_var_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_u64p, c_i32p]),
 }

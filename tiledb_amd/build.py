@@ -32,8 +32,7 @@ ARCH = os.environ.get("TDBG_ARCH", "gfx950")
 NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART_HOST)
 # (source, object name, extra flags)
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
-          ("tdbg_forward.hip", "tdbg_forward", []), ("tdbg_stream.hip", "tdbg_stream", []),
-          ("tdbg_stream_raw.hip", "tdbg_stream_raw", []),
+          ("tdbg_forward.hip", "tdbg_forward", []),
           ("tdbg_c5tile.hip", "tdbg_c5tile", []),
           ("tdbg_c2tile.hip", "tdbg_c2tile", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
@@ -50,6 +49,11 @@ UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_
           ("tdbg_cpu.cpp", "tdbg_cpu", ["-ffp-contract=off"])] +
          [("tdbg_fast.hip", f"tdbg_fast_p{k}", [f"-DTDBG_PART={k}", f"-DTDBG_NPART={NPART}"])
           for k in range(NPART)])
+# Retired C5 kernels (round 4's persistent coded-DD and raw-DD streaming
+# kernels, replaced by tdbg_c5tile.hip): only in the experiments library, for
+# same-box A/Bs through TDBG_C5_OLD_RAW; the product library does not contain
+# them.
+EXP_ONLY_UNITS = [("tdbg_stream.hip", "tdbg_stream", []), ("tdbg_stream_raw.hip", "tdbg_stream_raw", [])]
 HOST_ONLY = {"tdbg_cpu.cpp"}
 NO_SCRATCH = {"tdbg_stream.hip", "tdbg_stream_raw.hip", "tdbg_stream_small.hip", "tdbg_c5tile.hip",
               "tdbg_c2tile.hip"}  # checked with -Rpass-analysis
@@ -174,7 +178,7 @@ def _build_exp(force: bool, verbose: bool) -> str:
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}",
               "-I", os.path.join(ROOT, "include"), "-DTDBG_EXPERIMENTS"]
     jobs, objs = [], []
-    for src, name, extra in UNITS:
+    for src, name, extra in UNITS + EXP_ONLY_UNITS:
         if src not in HOOK_UNITS:
             objs.append(os.path.join(objdir, name + ".o"))
             continue

@@ -55,7 +55,6 @@ constexpr uint32_t OUTB = 65536;
 constexpr uint32_t IMGU = 4256;  // 16-B units of the image stage (68,096 B)
 constexpr uint32_t IMG_CAP = IMGU * 16 - 15;
 constexpr uint32_t TABN = 320;
-constexpr uint32_t OFFM = (1u << 20) - 1;
 constexpr uint32_t GRID_CAP = 1u << 22;
 constexpr uint32_t PFX = 192;  // 16-B units of the image prefix the parse reads (3 KiB)
 
@@ -68,15 +67,6 @@ struct Lds {
 // a 16-B unit at a 4-B aligned address (global_store_dwordx4 needs no more)
 typedef uint32_t v4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
 typedef __attribute__((address_space(1))) v4a g_a4;
-
-__device__ __forceinline__ uint32_t rd32(const uint32_t* a, uint32_t o) {
-  return __builtin_amdgcn_alignbyte(a[(o >> 2) + 1], a[o >> 2], o & 3);
-}
-
-template <bool SGN>
-__device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
-  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
-}
 
 __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
   if (threadIdx.x == 0) {
@@ -117,43 +107,8 @@ __device__ __forceinline__ void parse(Lds& L, uint32_t b, uint64_t fs, uint32_t 
   ok = ok && Lb == os && nwr >= 1 && nwr <= TABN && ml == 8 + 9 * nwr + bml && ws >= 256 && ws <= 4096 &&
        (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwr;
   const uint32_t nwin = ok ? nwr : 1;
-  const uint32_t e0 = m + 8 + 45 * l;
-  uint32_t R[13];
-#pragma unroll
-  for (int k = 0; k < 13; k++) R[k] = P[(e0 >> 2) + k];
-  const uint32_t sh = e0 & 3;
-  auto rw = [&](int o) -> uint32_t {
-    const uint32_t lo0 = R[o >> 2], hi0 = R[(o >> 2) + 1], hi1 = R[(o >> 2) + 2];
-    const uint32_t s = sh + (uint32_t)(o & 3);
-    return s < 4 ? __builtin_amdgcn_alignbyte(hi0, lo0, s) : __builtin_amdgcn_alignbyte(hi1, hi0, s - 4);
-  };
-  uint32_t cs[5], kind[5], mn[5];
-  bool bad = false;
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    const uint32_t wi = 5 * l + q;
-    const uint32_t vmin = rw(9 * q), bits = rw(9 * q + 4) & 0xffu, nb = rw(9 * q + 5);
-    const bool in = wi < nwin;
-    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
-    bad = bad || (in && nb != want);
-    const bool raw = bits >= 32 || (nb & 3) != 0;
-    bad = bad || (in && !raw && bits != 8 && bits != 16);
-    kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
-    cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
-    mn[q] = raw ? 0 : vmin;
-  }
-  const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
-  const uint32_t inc = wave_incscan_u32(s5);
-  ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
   const uint32_t dst = 20 + ml;  // image offset (from b) of the BWR data
-  {
-    uint32_t off = dst + inc - s5;
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kind[q] << 20), mn[q]);
-      off += cs[q];
-    }
-  }
+  ok = ok && bwr_window_table(P, L.TAB, m + 8 + 45 * l, nwin, ws, Lb, fl, dst, l).ok;
   // the bitshuffle md after the windows' headers
   ok = ok && bmd_ok(m + 8 + 9 * nwin);
   if (l == 0) {
@@ -162,54 +117,6 @@ __device__ __forceinline__ void parse(Lds& L, uint32_t b, uint64_t fs, uint32_t 
     L.hd[2] = nwin - 1;
     L.hd[3] = 0;  // (the stream is decoded to LDS byte 0)
   }
-}
-
-// (A/B, experiments build) BWR^-1 of the 64 KiB stream into LDS, in place
-// over the image, as a pass of its own: thread T
-// decodes 16-B units T + 1024 j (four elements, one window), per round one
-// wave-uniform decoder (all-8-bit: one dword; else per element by kind)
-template <bool SGN>
-__device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w,
-                                                uint32_t l) {
-  v4u dv[4];
-  uint2 te[4];
-  uint32_t ea[4];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t e = 4 * (1024 * j + 64 * w + l);
-    uint32_t W = e >> esh;
-    W = W < wlast ? W : wlast;
-    te[j] = L.TAB[W];
-    const uint32_t kind = te[j].x >> 20;
-    ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);
-  }
-  uint32_t D[4][5];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t* p = L.IMG + (ea[j] >> 2);
-#pragma unroll
-    for (int k = 0; k < 5; k++) D[j][k] = p[k];
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
-    if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
-      const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
-      dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
-    } else {
-      const uint32_t r0 = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh), r1 = __builtin_amdgcn_alignbyte(D[j][2], D[j][1], sh);
-      const uint32_t r2 = __builtin_amdgcn_alignbyte(D[j][3], D[j][2], sh), r3 = __builtin_amdgcn_alignbyte(D[j][4], D[j][3], sh);
-      const bool b8 = kind == 0, raw = kind == 2;
-      const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
-      const uint32_t e1 = ext<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
-      const uint32_t e2 = ext<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
-      const uint32_t e3 = ext<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
-      dv[j] = v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
-    }
-  }
-  lds_barrier();  // every compressed byte is in registers
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
 }
 
 __device__ __forceinline__ void tr4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t (&o)[4]) {
@@ -244,7 +151,7 @@ __device__ __forceinline__ void c2_body(Lds& L, uint8_t* out, uint32_t b, uint32
   // BWR^-1 of the whole stream into LDS first, as its own pass (tile-uniform)
   const bool mat = MODE == 1 && (MAT || R != 256);
   if (mat) {
-    bwr_materialize<SGN>(L, b, wsh - 2, wlast, w, l);
+    bwr_materialize<SGN>(L.IMG, L.TAB, b, wsh - 2, wlast, w, l, 4096);
     lds_barrier();  // the bitshuffled stream at LDS byte 0
   }
   // BWR-output element e (C2i, decoded from its window; any lane)

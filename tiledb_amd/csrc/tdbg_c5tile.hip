@@ -66,7 +66,6 @@ constexpr uint32_t IMGU = 4256;       // 16-B units of the image stage (68,096 B
 constexpr uint32_t IMG_CAP = IMGU * 16 - 15;
 constexpr uint32_t TABN = 320;        // BWR windows per chunk (nwin <= 257 for windows >= 256 B)
 constexpr uint32_t LBWR = 65562;      // BWR output bytes of a raw-DD C5 chunk: 17 + 9 + 65536
-constexpr uint32_t OFFM = (1u << 20) - 1;
 constexpr uint32_t GRID_CAP = 1u << 22;
 constexpr uint32_t PFX = 192;         // 16-B units of the image prefix the parse reads (3 KiB)
 
@@ -76,16 +75,6 @@ struct Lds {
   uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1, Lb, values
   uint32_t red[16][2];  // coded tiles: each wave's DD aggregate (A, B)
 };
-
-// bytes [o, o + 4) of a dword array (any alignment)
-__device__ __forceinline__ uint32_t rd32(const uint32_t* a, uint32_t o) {
-  return __builtin_amdgcn_alignbyte(a[(o >> 2) + 1], a[o >> 2], o & 3);
-}
-
-template <bool SGN>
-__device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
-  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
-}
 
 // the tile's shape is one this kernel decodes (descriptor checks only)
 // (a chunk of 4 n bytes, 16 <= n <= 16384 values; the output 4-B aligned)
@@ -139,11 +128,8 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
   const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
   const uint32_t m = b + ho + 12;
   const uint32_t e0 = m + 8 + 45 * l;  // m + 8 + 45 * 63 + 52 < 3,000
-  // ---- round 1
-  uint32_t R[13];
-#pragma unroll
-  for (int k = 0; k < 13; k++) R[k] = P[(e0 >> 2) + k];
-  // (uniform addresses: broadcast reads)
+  // ---- round 1 (the window headers are read inside bwr_window_table; the
+  // uniform addresses below are broadcast reads)
   const uint32_t nlo = rd32(P, b), nhi = rd32(P, b + 4), orig = rd32(P, b + ho), fl = rd32(P, b + ho + 4),
                  ml = rd32(P, b + ho + 8);
   const uint32_t Lb = rd32(P, m), nwr = rd32(P, m + 4), ws = rd32(P, m + 13);  // ws: window 0's byte count
@@ -152,48 +138,15 @@ __device__ __forceinline__ void parse(Lds& L, const Desc& d, uint32_t l, bool ch
             nwr <= TABN && ml == 8 + 9 * nwr + 24 && Lb <= LBWR && Lb >= 34 + 8 && ws >= 256 && ws <= 4096 &&
             (ws & (ws - 1)) == 0 && (Lb - 1) / ws + 1 == nwr;
   const uint32_t nwin = ok ? nwr : 2;
-  // window q's header: [T min][u8 bits][u32 bytes] at e0 + 9 q
-  const uint32_t sh = e0 & 3;
-  // (the byte shift sh + (o & 3) may reach 6: alignbyte takes it mod 4, so
-  // the dword index steps by hand)
-  auto rw = [&](int o) -> uint32_t {
-    const uint32_t lo0 = R[o >> 2], hi0 = R[(o >> 2) + 1], hi1 = R[(o >> 2) + 2];
-    const uint32_t s = sh + (uint32_t)(o & 3);
-    return s < 4 ? __builtin_amdgcn_alignbyte(hi0, lo0, s) : __builtin_amdgcn_alignbyte(hi1, hi0, s - 4);
-  };
-  uint32_t cs[5], kind[5], mn[5];
-  bool bad = false;
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    const uint32_t wi = 5 * l + q;
-    const uint32_t vmin = rw(9 * q), bits = rw(9 * q + 4) & 0xffu, nb = rw(9 * q + 5);
-    const bool in = wi < nwin;
-    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
-    bad = bad || (in && nb != want);
-    const bool raw = bits >= 32 || (nb & 3) != 0;
-    bad = bad || (in && !raw && bits != 8 && bits != 16);
-    kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
-    cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
-    mn[q] = raw ? 0 : vmin;
-  }
-  const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
-  const uint32_t inc = wave_incscan_u32(s5);
-  ok = ok && !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
   const uint32_t dst = ho + 12 + ml;  // image offset of the BWR data
-  {
-    uint32_t off = dst + inc - s5;
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-      if (5 * l + q < nwin) L.TAB[5 * l + q] = make_uint2(off | (kind[q] << 20), mn[q]);
-      off += cs[q];
-    }
-  }
+  const WinTab wt = bwr_window_table(P, L.TAB, e0, nwin, ws, Lb, fl, dst, l);
+  ok = ok && wt.ok;
   // ---- round 2: the compression frame md (compression_filter.cc:413-486):
   // 1 md part of 8 B (the byteshuffle header) compressed to 17 B, 1 data part
   // of os bytes compressed to d5 bytes (the BWR output is c0 + c1); the DD
   // headers = BWR-output bytes [0, 34): lane e decodes element e < 9 of
   // window 0
-  const uint32_t k0 = __builtin_amdgcn_readfirstlane(kind[0]), mn0 = __builtin_amdgcn_readfirstlane(mn[0]);
+  const uint32_t k0 = wt.k0, mn0 = wt.mn0;
   const uint32_t f = m + 8 + 9 * nwin;
   const uint32_t lf = l < 6 ? l : 5;
   const uint32_t fv = rd32(P, f + 4 * lf);  // lane i < 6: frame dword i
@@ -455,70 +408,6 @@ __device__ __forceinline__ void scan_step(uint32_t& A, uint32_t& B, uint32_t nse
   A = A + Ap;
 }
 
-// BWR^-1 of the whole chunk (bit_width_reduction_filter.cc:353-404) into LDS,
-// in place over the image, in 16-B units of 4 elements: thread T decodes
-// units T + 1024 j (j < 4: the coded BWR output is at most 63,514 B = 3,970
-// units).  A unit's 4 elements lie in one window (windows are >= 64
-// elements), looked up per lane.  Per round one wave-uniform decoder: every
-// lane's window 8-bit (most rounds of an active tile: one dword read gives
-// the unit), or the general form (five dwords realigned, then per element
-// the window's kind: raw dword, 8-bit byte or 16-bit half, plus the
-// minimum).  Every compressed read lands in registers before the one
-// barrier after which the decoded units overwrite the image.
-template <bool SGN>
-__device__ __forceinline__ void bwr_materialize(Lds& L, uint32_t b, uint32_t esh, uint32_t wlast, uint32_t w,
-                                                uint32_t l, uint32_t nun) {
-  v4u dv[4];
-  uint2 te[4];
-  uint32_t ea[4];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t e = 4 * (1024 * j + 64 * w + l);
-    uint32_t W = e >> esh;
-    W = W < wlast ? W : wlast;
-    te[j] = L.TAB[W];
-    const uint32_t kind = te[j].x >> 20;
-    ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);  // LDS byte of element e's compressed value
-  }
-  // (every round's five dwords first, so that all 20 reads are in flight
-  // together; the decoders below pick from them)
-  // (rounds whose units all lie past the BWR output, nun units, are skipped:
-  // a wave-uniform test)
-  uint32_t D[4][5];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
-    const uint32_t* p = L.IMG + (ea[j] >> 2);
-#pragma unroll
-    for (int k = 0; k < 5; k++) D[j][k] = p[k];
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
-    const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
-    if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
-      const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
-      dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
-    } else {
-      const uint32_t r0 = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh), r1 = __builtin_amdgcn_alignbyte(D[j][2], D[j][1], sh);
-      const uint32_t r2 = __builtin_amdgcn_alignbyte(D[j][3], D[j][2], sh), r3 = __builtin_amdgcn_alignbyte(D[j][4], D[j][3], sh);
-      const bool b8 = kind == 0, raw = kind == 2;
-      // element i: 8-bit -> byte i of r0; 16-bit -> half (i & 1) of r(i >> 1)
-      const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
-      const uint32_t e1 = ext<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
-      const uint32_t e2 = ext<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
-      const uint32_t e3 = ext<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
-      dv[j] = v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
-    }
-  }
-  lds_barrier();  // every compressed byte is in registers: the stream may overwrite the image
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
-    *(v4u*)(L.IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
-  }
-}
-
 // The lane's 16 values (local running sums) and its exclusive wave prefix
 // (ae, be); lane 63 publishes the wave total.
 template <int CB>
@@ -588,7 +477,7 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
   const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
   uint32_t xk[16], ae, be;
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  bwr_materialize<SGN>(L, b, esh, wlast, w, l, (__builtin_amdgcn_readfirstlane(L.hd[6]) + 15) >> 4);
+  bwr_materialize<SGN>(L.IMG, L.TAB, b, esh, wlast, w, l, (__builtin_amdgcn_readfirstlane(L.hd[6]) + 15) >> 4);
   lds_barrier();  // the decoded stream
   coded_lane<CB>(L, w, l, x0, x1, xk, ae, be, nv);
   const uint64_t c4 = prof ? __builtin_amdgcn_s_memtime() : 0;

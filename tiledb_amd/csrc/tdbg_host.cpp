@@ -62,10 +62,14 @@ static hipError_t tdbg_launch_fast(const tdbg::KParams* kp, uint32_t grid, hipSt
   return parts[kp->plan.fast % TDBG_NPART_HOST](kp, grid, stream);
 }
 extern "C" uint32_t tdbg_fast_select(const tdbg_plan* plan);
+#ifdef TDBG_EXPERIMENTS
+// the retired round-4 C5 streaming kernels (experiments library only: A/B
+// through TDBG_C5_OLD_RAW)
 extern "C" hipError_t tdbg_launch_stream(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
+#endif
 extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_c2tile(const tdbg::KParams* kp, int mode, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
@@ -199,6 +203,8 @@ struct tdbg_context {
   uint32_t* dense_err = nullptr;  // set by the var sizes kernel: offsets outside their var tile
   uint8_t* dv_arena = nullptr;    // tdbg_dense_read_var_host's device buffers (grow-only)
   uint64_t dv_cap = 0;
+  uint8_t* dv_extra = nullptr;    // its var result when overlapping offsets outgrow the carve (grow-only)
+  uint64_t dv_extra_cap = 0;
   uint32_t fwd_retry_caps[3] = {0, 0, 0};  // diagnostics: largest retry slot
   // per-tile status / need
   int32_t* d_status = nullptr;
@@ -608,6 +614,7 @@ void tdbg_context_destroy(tdbg_context* c) {
   if (c->dense_bsum) (void)hipFree(c->dense_bsum);
   if (c->dense_err) (void)hipFree(c->dense_err);
   if (c->dv_arena) (void)hipFree(c->dv_arena);
+  if (c->dv_extra) (void)hipFree(c->dv_extra);
   for (auto& s : c->st) {
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
@@ -671,7 +678,8 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   {
     static const bool prof = tdbg_hook("TDBG_PROF") != nullptr;
     if (prof && fast) {
-      const uint32_t pgrid = std::max<uint32_t>(grid, tdbg_stream_grid(c->cus));
+      // (rows for every workgroup < 1024 of the tile kernels; the fused grid)
+      const uint32_t pgrid = std::max<uint32_t>(grid, 1024u);
       if (c->prof_grid < pgrid) {
         if (c->d_prof) (void)hipFree(c->d_prof);
         c->d_prof = nullptr;
@@ -705,7 +713,9 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // integers (fused specs 19/20) first goes through the streaming kernel
   // (tdbg_stream.hip); the fused kernel then runs on the tiles it left.
   static const bool no_stream = tdbg_hook("TDBG_NO_STREAM") != nullptr;  // ablation
+#ifdef TDBG_EXPERIMENTS
   static const bool c5_old_raw = tdbg_hook("TDBG_C5_OLD_RAW") != nullptr;  // A/B: the persistent raw-DD kernel
+#endif
   const bool c5_stream = (p->plan.fast == 19 || p->plan.fast == 20) && p->plan.nstages == 3 &&
                          p->plan.s[2].dts == 4 && p->plan.s[1].w == 4;
   // The scan pipelines of C3a / C3b / C4 on 8-byte values first go through
@@ -828,11 +838,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
     } else {
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
+#ifdef TDBG_EXPERIMENTS
       if (c5_old_raw) {
         if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
         if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
         if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
-      } else if (!skip_fused) {
+      } else
+#endif
+      if (!skip_fused) {
         e = tdbg_launch_c5tile(&ks, sgn, stream);
       }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
@@ -871,11 +884,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("small stream kernel launch: ") + hipGetErrorString(e));
     } else {
       const int sgn = p->plan.s[2].sgn ? 1 : 0;
+#ifdef TDBG_EXPERIMENTS
       if (c5_old_raw) {
         if (!skip_fused) e = tdbg_launch_stream(&ks, tdbg_stream_grid(c->cus), sgn, stream);
         if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("stream kernel launch: ") + hipGetErrorString(e));
         if (!skip_fused) e = tdbg_launch_stream_raw(&ks, tdbg_stream_raw_grid(c->cus), sgn, stream);
-      } else if (!skip_fused) {
+      } else
+#endif
+      if (!skip_fused) {
         e = tdbg_launch_c5tile(&ks, sgn, stream);
       }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
@@ -2137,10 +2153,9 @@ int tdbg_dense_var_offsets_async(tdbg_context* c, const tdbg_dense_frag_config* 
   HIP_OK(hipSetDevice(c->device));
   int rc = order_stream(c, (hipStream_t)stream);
   if (rc) return rc;
-  if (!c->dense_err) {
-    HIP_OK(hipMalloc(&c->dense_err, 4));
-    HIP_OK(hipMemsetAsync(c->dense_err, 0, 4, (hipStream_t)stream));
-  }
+  if (!c->dense_err) HIP_OK(hipMalloc(&c->dense_err, 4));
+  // (per call, ordered with this call's kernel on the caller's stream)
+  HIP_OK(hipMemsetAsync(c->dense_err, 0, 4, (hipStream_t)stream));
   const uint64_t n = dense_cells(&cfg->base);
   const uint64_t nb = (n + 2047) / 2048;
   if (n > c->dense_src_cap) {
@@ -2180,6 +2195,17 @@ int tdbg_dense_var_copy_async(tdbg_context* c, const tdbg_dense_frag_config* cfg
                                             cfg->elements_mode ? cfg->data_type_size : 1, d_result_var, grid,
                                             (hipStream_t)stream);
   if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("dense var copy launch: ") + hipGetErrorString(e));
+  return TDBG_OK;
+}
+
+int tdbg_dense_var_status(tdbg_context* c, tdbg_stream stream, int32_t* status) {
+  if (!c || !status) return fail(TDBG_E_ARG, "null context or status");
+  if (!c->dense_err) return fail(TDBG_E_ARG, "tdbg_dense_var_status: no tdbg_dense_var_offsets_async on this context");
+  HIP_OK(hipSetDevice(c->device));
+  uint32_t herr = 0;
+  HIP_OK(hipMemcpyAsync(&herr, c->dense_err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  *status = herr ? TDBG_E_DATA_READ : TDBG_OK;
   return TDBG_OK;
 }
 
@@ -2373,17 +2399,27 @@ int tdbg_dense_read_var_host(tdbg_context* c, const tdbg_pipeline* po, const tdb
   uint32_t herr = 0;
   HIP_OK(hipMemcpyAsync(&herr, c->dense_err, 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
-  if (herr) {
-    HIP_OK(hipMemset(c->dense_err, 0, 4));
-    return fail(TDBG_E_DATA_READ, "dense var read: a cell's offsets lie outside its var tile");
-  }
+  if (herr) return fail(TDBG_E_DATA_READ, "dense var read: a cell's offsets lie outside its var tile");
   const uint64_t mult = cfg->elements_mode ? cfg->data_type_size : 1;
   const uint64_t vbytes = *var_total * mult;
   if (vbytes > var_cap || (vbytes && !result_var))
     return fail(TDBG_E_OUT_FULL, "dense var read: var buffer too small");
   if (vbytes) {
-    if (vbytes > rvar_max) return fail(TDBG_E_INTERNAL, "dense var read: result bound");
-    uint8_t* const d_rvar = d_rvar_region;  // (rvar_max bytes, carved above)
+    uint8_t* d_rvar = d_rvar_region;  // (rvar_max bytes, carved above)
+    if (vbytes > rvar_max) {
+      // overlapping (but in-bounds) cell offsets can read a var tile's bytes
+      // more than once: the result outgrows the carve, never var_cap; a
+      // grow-only buffer of its own (the arena's other carves are in use)
+      if (vbytes > c->dv_extra_cap) {
+        if (c->dv_extra) (void)hipFree(c->dv_extra);
+        c->dv_extra = nullptr;
+        c->dv_extra_cap = 0;
+        if (hipMalloc(&c->dv_extra, vbytes) != hipSuccess)
+          return fail(TDBG_E_DEVICE, "dense var read: device allocation failed");
+        c->dv_extra_cap = vbytes;
+      }
+      d_rvar = c->dv_extra;
+    }
     rc = tdbg_dense_var_copy_async(c, &g, d_roff, d_total, d_rvar, s);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(result_var, d_rvar, vbytes, hipMemcpyDeviceToHost, s));

@@ -1,12 +1,14 @@
-// tdbg_stream_common.h -- pieces shared by the streaming C5 kernels
-// (tdbg_stream.hip: DoubleDelta bit-packed; tdbg_stream_raw.hip: DoubleDelta
-// raw): persistent-grid tile walk with descriptors batched 64 at a time, the
-// LDS-DMA of 16-B units, and the LDS-only workgroup barrier.
+// tdbg_stream_common.h -- pieces shared by the streaming / tile kernels
+// (tdbg_c5tile.hip, tdbg_c2tile.hip, tdbg_stream_small.hip, and the retired
+// tdbg_stream*.hip of the experiments build): tile descriptors, the LDS-DMA
+// of 16-B units, the LDS-only workgroup barrier, and the tile kernels' BWR
+// window table and in-LDS BWR^-1.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "tdbg_desc.h"
+#include "tdbg_device.h"
 
 namespace tdbg {
 namespace sc {
@@ -138,6 +140,142 @@ __device__ __forceinline__ void dma16(uint64_t src, uint32_t dst_wave) {
 // Workgroup barrier for LDS only: no vmcnt drain (outstanding stores and the
 // next tile's DMA stay in flight); "memory" keeps LDS accesses on their side.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// Pieces of the one-workgroup-per-tile kernels (tdbg_c5tile.hip,
+// tdbg_c2tile.hip): the whole filtered image staged in LDS as dwords, BWR
+// windows described by a table of {image offset of the window's data |
+// kind << 20, window minimum} (kind 0: 8-bit, 1: 16-bit, 2: raw)
+// ---------------------------------------------------------------------------
+constexpr uint32_t OFFM = (1u << 20) - 1;
+
+// bytes [o, o + 4) of a dword array (any alignment)
+__device__ __forceinline__ uint32_t rd32(const uint32_t* a, uint32_t o) {
+  return __builtin_amdgcn_alignbyte(a[(o >> 2) + 1], a[o >> 2], o & 3);
+}
+
+// bits [o, o + w) of x, sign- or zero-extended (BWR's stored values are
+// signed for signed T, bit_width_reduction_filter.cc:491-528)
+template <bool SGN>
+__device__ __forceinline__ uint32_t ext(uint32_t x, uint32_t o, uint32_t w) {
+  return SGN ? (uint32_t)__builtin_amdgcn_sbfe((int32_t)x, o, w) : __builtin_amdgcn_ubfe(x, o, w);
+}
+
+// The BWR window table of a chunk (one wave): window q's header [T min][u8
+// bits][u32 bytes] sits at image byte e0 - 45 l + 9 q (lane l reads windows
+// 5 l .. 5 l + 4, 45 bytes from e0); window sizes must be ws except the last
+// (Lb bytes in all), stored widths 8 / 16 or raw (bits >= 32, or a byte count
+// that is not a multiple of 4: bit_width_reduction_filter.cc:353-404); the
+// compressed sizes' DPP scan places each window's data from image byte dst.
+// Returns false (every lane) when a header is off or the sizes do not sum to
+// fl; TAB[0 .. nwin) is written either way.  k0 / mn0: window 0's kind and
+// minimum (lane 0's).
+struct WinTab {
+  bool ok;
+  uint32_t k0, mn0;
+};
+__device__ __forceinline__ WinTab bwr_window_table(const uint32_t* P, uint2* TAB, uint32_t e0, uint32_t nwin,
+                                                   uint32_t ws, uint32_t Lb, uint32_t fl, uint32_t dst, uint32_t l) {
+  uint32_t R[13];
+#pragma unroll
+  for (int k = 0; k < 13; k++) R[k] = P[(e0 >> 2) + k];
+  const uint32_t sh = e0 & 3;
+  // (the byte shift sh + (o & 3) may reach 6: alignbyte takes it mod 4, so
+  // the dword index steps by hand)
+  auto rw = [&](int o) -> uint32_t {
+    const uint32_t lo0 = R[o >> 2], hi0 = R[(o >> 2) + 1], hi1 = R[(o >> 2) + 2];
+    const uint32_t s = sh + (uint32_t)(o & 3);
+    return s < 4 ? __builtin_amdgcn_alignbyte(hi0, lo0, s) : __builtin_amdgcn_alignbyte(hi1, hi0, s - 4);
+  };
+  uint32_t cs[5], kind[5], mn[5];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint32_t wi = 5 * l + q;
+    const uint32_t vmin = rw(9 * q), bits = rw(9 * q + 4) & 0xffu, nb = rw(9 * q + 5);
+    const bool in = wi < nwin;
+    const uint32_t want = wi + 1 < nwin ? ws : Lb - ws * (nwin - 1);
+    bad = bad || (in && nb != want);
+    const bool raw = bits >= 32 || (nb & 3) != 0;
+    bad = bad || (in && !raw && bits != 8 && bits != 16);
+    kind[q] = raw ? 2 : bits == 8 ? 0 : 1;
+    cs[q] = !in ? 0 : raw ? nb : bits == 8 ? nb >> 2 : nb >> 1;
+    mn[q] = raw ? 0 : vmin;
+  }
+  const uint32_t s5 = cs[0] + cs[1] + cs[2] + cs[3] + cs[4];
+  const uint32_t inc = wave_incscan_u32(s5);
+  const bool ok = !__builtin_amdgcn_ballot_w64(bad) && __builtin_amdgcn_readlane(inc, 63) == fl;
+  uint32_t off = dst + inc - s5;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    if (5 * l + q < nwin) TAB[5 * l + q] = make_uint2(off | (kind[q] << 20), mn[q]);
+    off += cs[q];
+  }
+  return WinTab{ok, (uint32_t)__builtin_amdgcn_readfirstlane(kind[0]), (uint32_t)__builtin_amdgcn_readfirstlane(mn[0])};
+}
+
+// BWR^-1 of a whole chunk's stream (bit_width_reduction_filter.cc:353-404)
+// into LDS, in place over the image, in 16-B units of 4 elements: thread T of
+// a 1,024-thread workgroup decodes units T + 1024 j (j < 4: at most 64 KiB of
+// output; rounds whose units all lie past nun units are skipped, a
+// wave-uniform test).  A unit's 4 elements lie in one window (windows are >=
+// 64 elements), looked up per lane (esh = log2(elements per window), wlast =
+// the last window).  Per round one wave-uniform decoder: every lane's window
+// 8-bit (one dword read gives the unit), or the general form (five dwords
+// realigned, then per element the window's kind: raw dword, 8-bit byte or
+// 16-bit half, plus the minimum).  Every compressed read lands in registers
+// before the one barrier after which the decoded units overwrite the image.
+template <bool SGN>
+__device__ __forceinline__ void bwr_materialize(uint32_t* IMG, const uint2* TAB, uint32_t b, uint32_t esh,
+                                                uint32_t wlast, uint32_t w, uint32_t l, uint32_t nun) {
+  v4u dv[4];
+  uint2 te[4];
+  uint32_t ea[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t e = 4 * (1024 * j + 64 * w + l);
+    uint32_t W = e >> esh;
+    W = W < wlast ? W : wlast;
+    te[j] = TAB[W];
+    const uint32_t kind = te[j].x >> 20;
+    ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);  // LDS byte of element e's compressed value
+  }
+  // (every round's five dwords first, so that all 20 reads are in flight
+  // together; the decoders below pick from them)
+  uint32_t D[4][5];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
+    const uint32_t* p = IMG + (ea[j] >> 2);
+#pragma unroll
+    for (int k = 0; k < 5; k++) D[j][k] = p[k];
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
+    const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
+    if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
+      const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
+      dv[j] = v4u{ext<SGN>(y, 0, 8) + mn, ext<SGN>(y, 8, 8) + mn, ext<SGN>(y, 16, 8) + mn, ext<SGN>(y, 24, 8) + mn};
+    } else {
+      const uint32_t r0 = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh), r1 = __builtin_amdgcn_alignbyte(D[j][2], D[j][1], sh);
+      const uint32_t r2 = __builtin_amdgcn_alignbyte(D[j][3], D[j][2], sh), r3 = __builtin_amdgcn_alignbyte(D[j][4], D[j][3], sh);
+      const bool b8 = kind == 0, raw = kind == 2;
+      // element i: 8-bit -> byte i of r0; 16-bit -> half (i & 1) of r(i >> 1)
+      const uint32_t e0 = ext<SGN>(r0, 0, b8 ? 8 : 16) + mn;
+      const uint32_t e1 = ext<SGN>(r0, b8 ? 8 : 16, b8 ? 8 : 16) + mn;
+      const uint32_t e2 = ext<SGN>(b8 ? r0 : r1, b8 ? 16 : 0, b8 ? 8 : 16) + mn;
+      const uint32_t e3 = ext<SGN>(b8 ? r0 : r1, b8 ? 24 : 16, b8 ? 8 : 16) + mn;
+      dv[j] = v4u{raw ? r0 : e0, raw ? r1 : e1, raw ? r2 : e2, raw ? r3 : e3};
+    }
+  }
+  lds_barrier();  // every compressed byte is in registers: the stream may overwrite the image
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    if (1024 * j + 64 * w >= nun) break;
+    *(v4u*)(IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+  }
+}
 
 }  // namespace sc
 }  // namespace tdbg

@@ -508,6 +508,15 @@ def dense_var_copy_async(ctx, fcfg, d_result_offsets, d_var_total, d_result_var,
                                          ctx._stream(stream)), "tdbg_dense_var_copy_async")
 
 
+def dense_var_status(ctx, stream=None) -> int:
+    """tdbg_dense_var_status: the data check of the context's last
+    dense_var_offsets_async (TDBG_OK, or TDBG_E_DATA_READ when a cell's
+    offsets lay outside its var tile); waits for `stream`."""
+    st = ctypes.c_int32(0)
+    _check(lib.tdbg_dense_var_status(ctx.h, ctx._stream(stream), ctypes.byref(st)), "tdbg_dense_var_status")
+    return int(st.value)
+
+
 def dense_read_var_host(ctx, dp_off: DevicePipeline, dp_var: DevicePipeline, fcfg, tile_start, frag_dom,
                         off_filtered, var_filtered, var_unfiltered_size, fill_value: bytes, var_cap: int,
                         out_offsets=None, out_var=None):

@@ -9,7 +9,7 @@ V=${2:-varlibs/pw.so}
 OUT=$R/gpurun_out/raw_ab_$TAG
 mkdir -p $OUT
 cd $R
-TDBG_LIB=$V timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_stream.py tests/test_gpu_stream_small.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 120 \
+TDBG_LIB=$V timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_c5tile.py tests/test_gpu_stream_small.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 120 \
   --timeout-method thread > $OUT/pytest_variant.log 2>&1 || { echo "variant parity failed"; tail -30 $OUT/pytest_variant.log; exit 11; }
 tail -1 $OUT/pytest_variant.log
 for rep in 1 2; do

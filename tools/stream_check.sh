@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/stream_${1:-x}
 mkdir -p $OUT
 cd $R
-timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_stream.log 2>&1 || { echo "stream tests failed"; tail -40 $OUT/pytest_stream.log; exit 11; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_c5tile.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_stream.log 2>&1 || { echo "stream tests failed"; tail -40 $OUT/pytest_stream.log; exit 11; }
 tail -3 $OUT/pytest_stream.log
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "c5 or C5 or spec19 or spec20" > $OUT/pytest_c5.log 2>&1 || { echo "c5 parity failed"; tail -40 $OUT/pytest_c5.log; exit 12; }
 tail -2 $OUT/pytest_c5.log
