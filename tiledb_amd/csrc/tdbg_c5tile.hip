@@ -562,7 +562,8 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
 
 // ABL (timing ablations, outputs not meaningful): 1 no parse and no decode
 // (DMA, barriers, constant stores), 2 parse but no decode, 3 no stores,
-// 4 every wave on the one-read path, 5 no 8-bit combine
+// 4 every wave on the one-read path, 5 no 8-bit combine, 6 two halves of 8
+// one-read ranges
 template <bool SGN, int ABL>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
@@ -684,7 +685,9 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   // The few general ranges (a wave of a ramp tile on a plane boundary) take
   // the per-element decoder under a wave-uniform branch that holds no LDS
   // access, so the reads stay in flight together (8 at a time in such waves,
-  // for registers).
+  // for registers).  (Measured, not kept: the general rounds first, one at a
+  // time, then all 16 one-read ranges together -- ramp -0.9 %, rand -1.1 %
+  // on one box, profiles/r06/ab_general_first.txt.)
   if (g.gen == 0 || ABL == 4) {
     decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
   } else if (ABL == 6) {
