@@ -60,9 +60,9 @@ CONFIGS = {
     "c5s": dict(tiles_per_gpu=163840, variants="active,rand,ramp", dtype="int32",
                 workload="C5 pipeline on 40,000-B tiles (10,000 int32 values, one chunk), 163,840 tiles "
                          "per GPU (the c5 leg's 6.55 GB of output)"),
-    "c5big": dict(tiles_per_gpu=200, variants="active", dtype="int32",
-                  workload="C5 pipeline, 4 MiB tiles (64 chunks of 64 KiB), 200 tiles per GPU: "
-                           "chunk-parallel launch (device chunk directory)"),
+    "c5big": dict(tiles_per_gpu=512, variants="active,rand,ramp", dtype="int32", unique=12,
+                  workload="C5 pipeline, 4 MiB tiles (64 chunks of 64 KiB), 512 tiles per GPU: tile mode "
+                           "(TDBG_MULTI_CHUNK: one workgroup walks a tile's chunks)"),
     # XOR / DELTA / FLOAT_SCALE pipelines (not BASELINE configs; tiles encoded
     # on the device by tdbg_filter_tiles, checked against the values)
     "xor": dict(tiles_per_gpu=10000, variants="sin", dtype="float32",
@@ -88,7 +88,9 @@ def build_batch(engine, cfg: str, variant: str, ntiles: int, nunique: int, devic
             raise SystemExit(f"{cfg}: device forward encode failed: {np.unique(st)}")
         return [t.tobytes() for t in tiles]
 
-    pool, vals = W.pool(cfg, variant, nunique, seed, encode=encode)
+    pool, vals = W.pool(cfg, variant, min(nunique, CONFIGS.get(cfg, {}).get("unique", nunique)), seed,
+                        encode=encode)
+    nunique = len(vals)
     vals = [W.expected(cfg, v) for v in vals]
     idx = np.arange(ntiles) % nunique
     sizes = np.array([len(pool[i]) for i in idx], dtype=np.uint64)
@@ -174,7 +176,7 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
         raise SystemExit(f"device status nonzero: {np.unique(st)}")
     fused0, fb0, _ = ctx.path_stats()
     s0 = ctx.stream_tiles()
-    c0 = ctx.stream_chunks()
+    c0 = ctx.stream_chunks() + ctx.tile_chunks()
     batch.d_status.fill_(-1)
 
     def timed(events: bool) -> float:
@@ -199,7 +201,7 @@ def time_device(engine, ctx, dp, batch, steps: int, warmup: int, dist, world: in
         raise SystemExit(f"timed launches: device status nonzero: {np.unique(st)}")
     fused1, fb1, _ = ctx.path_stats()
     s1 = ctx.stream_tiles()
-    c1 = ctx.stream_chunks()
+    c1 = ctx.stream_chunks() + ctx.tile_chunks()
     batch.d_status.fill_(-1)
     ev_elapsed = timed(True)
     kern_ms, total_ms = ctx.launch_times(steps)
@@ -469,8 +471,8 @@ def frac(r):
 
 def kernel_name(cfgname, r):
     if cfgname == "c5big" and r.get("stream_chunks"):
-        return ("chunk directory (dir_count/dir_scan/dir_fill) + unfilter_c5tile_kernel on chunk records + "
-                "unfilter_fused_kernel (queue of declined chunks)")
+        return ("unfilter_c5tile_kernel<MC> (tile mode: one workgroup per tile walks its chunks; or the chunk "
+                "directory's records) + unfilter_fused_kernel (queue of declined tiles)")
     if cfgname in ("c5", "c5s", "c5big") and r["streamed"]:
         return "unfilter_c5tile_kernel + unfilter_fused_kernel (queue of declined tiles)"
     if cfgname == "c1" and r["streamed"]:
@@ -891,6 +893,8 @@ def main():
                     help="N = 1 run: also time C5 on one GPU's shard of an 8-GPU node (100k / 8)")
     ap.add_argument("--c5s-tiles", type=int, default=CONFIGS["c5s"]["tiles_per_gpu"],
                     help="N = 1 run: also time the C5 pipeline on 40,000-B tiles (0 = skip)")
+    ap.add_argument("--c5big-tiles", type=int, default=CONFIGS["c5big"]["tiles_per_gpu"],
+                    help="N = 1 run: also time the C5 pipeline on 4 MiB tiles, tile mode (0 = skip)")
     ap.add_argument("--legs-file", default="gpurun_out/bench_legs.json",
                     help="every leg's full JSON (also printed on the line before the headline); '' = none")
     args = ap.parse_args()
@@ -991,6 +995,20 @@ def main():
                 "kernel": kernel_name("c5s", cres[variants[0]]), "variants": ss,
                 "min_over_variants_GiBps": round(min(x["GiBps"] for x in ss.values()), 2),
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in ss.values()), 4)}
+        # the C5 pipeline on 4 MiB tiles (64 chunks each): the everyday shape
+        # of dense tiles over 64 KiB (tile.cc:87-100), tile mode
+        if args.c5big_tiles:
+            sb = {}
+            _, cres = run_config(engine, ctx, W, args, "c5big", variants, args.c5big_tiles, args.steps,
+                                 args.warmup, dist, world, rank)
+            for v in variants:
+                sb[v] = variant_line("c5big", v, cres[v], world)
+                sb[v]["chunks_taken_per_launch"] = cres[v]["stream_chunks"] // max(1, args.steps)
+                cres[v].pop("packed", None)
+            line["config"]["c5_4MiB_tiles"] = {
+                "workload": CONFIGS["c5big"]["workload"], "tiles": args.c5big_tiles, "steps": args.steps,
+                "kernel": kernel_name("c5big", cres[variants[0]]), "variants": sb,
+                "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sb.values()), 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # after every timed region, at N = 1 only (the N > 1 lines divide the
         # same job over more GPUs; the CPU figure does not change with N)

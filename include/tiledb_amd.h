@@ -128,6 +128,16 @@ enum tdbg_status {
  * tiles.  Results and statuses are those of a tile launch.  Applied
  * automatically when a launch has fewer tiles than the device has CUs. */
 #define TDBG_CHUNK_PARALLEL 0x8u
+/* Some tile of the launch holds several chunks (an unfiltered size over the
+ * pipeline's 64 KiB chunks, tile.cc:87-100).  Tile-mode launches of the
+ * headline pipeline [BYTESHUFFLE, DOUBLE_DELTA, BIT_WIDTH_REDUCTION] on 4-byte
+ * integers then run the C5 tile kernel's multi-chunk variant, in which a
+ * workgroup decodes its tile's chunks one after the other
+ * (FilterPipeline::run_reverse's loop, filter_pipeline.cc:439-517); without it
+ * such tiles go to the fused kernel.  Results and statuses are the same
+ * either way.  The host-resident entries set it themselves from the tile
+ * sizes they are given. */
+#define TDBG_MULTI_CHUNK 0x10u
 /* tdbg_unfilter_tiles_host only: every input tile of the call lies in ONE host
  * allocation (e.g. a FilteredData block, filtered_data.h:152-644), so tiles
  * separated by at most 64 B of padding may move in one H2D copy (padding
@@ -335,6 +345,9 @@ int tdbg_context_stream_raw_stats(const tdbg_context* c, uint64_t* raw_tiles);
  * as the one-chunk tiles are).  Cumulative; waits for the context's last
  * launch. */
 int tdbg_context_stream_chunk_stats(const tdbg_context* c, uint64_t* chunks);
+/* Chunks of multi-chunk tiles the C5 tile kernel decoded in tile mode
+ * (TDBG_MULTI_CHUNK launches), cumulative per context. */
+int tdbg_context_tile_chunk_stats(const tdbg_context* c, uint64_t* chunks);
 /* Forward direction: tiles the LDS-resident forward kernels filtered --
  * [BYTESHUFFLE, DOUBLE_DELTA, BWR(256)] on INT32 / UINT32
  * (tdbg_forward_stream.hip) and, on 8-byte values, [DOUBLE_DELTA], [RLE] and

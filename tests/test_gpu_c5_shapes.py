@@ -215,3 +215,93 @@ def test_c5_short_last_chunks(eng, ctx, oracle_mod):
                                    [values(v, last, rng, 3)]))
     want, took, total = _chunk_mode(eng, ctx, oracle_mod, ser, Datatype.INT32, 4, vals, 14)
     assert want >= 14 * 15 and took == want
+
+
+# a tile-mode launch of multi-chunk tiles: at least two tiles per CU (fewer
+# go through the device chunk directory, tdbg_host.cpp launch())
+MC_TILES = 544
+
+
+def _mc_taken(f: np.ndarray) -> bool:
+    """The multi-chunk variant takes the tile: every chunk one the tile
+    kernel decodes (the tile is declined whole otherwise)."""
+    return all(chunk_taken(f, h) for h in _chunk_headers(f))
+
+
+def _mc_tile_mode(eng, ctx, O, case, n=MC_TILES, align=1):
+    """TDBG_MULTI_CHUNK tile-mode launch (the engine's default for tiles over
+    64 KiB) of n tiles cycling over the case's: bit-exact vs the oracle and
+    identical statuses; returns (expected chunks, chunks taken, tiles the
+    kernel should take, tiles the tile kernels took, fallback)."""
+    from tests.test_gpu_parity import check_parity_replicated, encode
+    import torch
+    assert n >= 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    _, enc = encode(O, case)
+    f0, b0, _ = ctx.path_stats()
+    s0, k0, c0 = ctx.stream_tiles(), ctx.tile_chunks(), ctx.stream_chunks()
+    check_parity_replicated(eng, ctx, O, case, enc, n, align=align, chunk_parallel=None)
+    f1, b1, _ = ctx.path_stats()
+    idx = np.arange(n) % len(enc)
+    want_tiles = sum(_mc_taken(enc[i][0]) for i in idx)
+    want_chunks = sum(len(_chunk_headers(enc[i][0])) for i in idx if _mc_taken(enc[i][0]))
+    assert ctx.stream_chunks() == c0, "tile mode expected, not the chunk directory"
+    return want_chunks, ctx.tile_chunks() - k0, want_tiles, ctx.stream_tiles() - s0, b1 - b0
+
+
+@pytest.mark.parametrize("align", [1, 16])
+def test_c5_multichunk_tile_mode(eng, ctx, oracle_mod, align):
+    """multi-chunk tiles in tile mode on the C5 tile kernel
+    (FilterPipeline::run_reverse's loop over chunks, filter_pipeline.cc:
+    439-517): 2, 3 and 4-chunk tiles, raw (rand, ramp) and coded (active,
+    step) chunks mixed inside a tile, short last chunks of every n mod 4.
+    Every tile whose chunks the kernel decodes is taken whole, chunk by
+    chunk (counter TDBG_STAT_TILE_CHUNKS); a tile with a chunk too small for
+    256-B windows goes to the fused kernel whole; bit-exact either way."""
+    rng = np.random.default_rng(707)
+    vals = []
+    for k, (kinds, last) in enumerate([(("rand", "active"), 16384), (("active", "ramp", "rand"), 16384),
+                                       (("ramp", "ramp"), 1001), (("step17", "active", "rand"), 4098),
+                                       (("rand", "rand", "active", "ramp"), 16383), (("active",), 2),
+                                       (("step3", "step30"), 40000 // 4 + 1)]):
+        parts = [values(v, 16384, rng, 8 * k + c) for c, v in enumerate(kinds)]
+        parts.append(values(kinds[-1], last, rng, 8 * k + 7))
+        vals.append(np.concatenate(parts))
+    case = Case("c5_mc", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
+    want_c, took_c, want_t, took_t, fb = _mc_tile_mode(eng, ctx, oracle_mod, case, align=align)
+    assert fb == 0
+    assert want_t < MC_TILES and want_t > MC_TILES // 2  # (the 2-value last chunk's tiles are declined)
+    assert took_c == want_c, f"took {took_c} chunks, expected {want_c}"
+    assert took_t == want_t
+
+
+def test_c5_multichunk_tile_mode_corrupt(eng, ctx, oracle_mod):
+    """Multi-chunk tiles whose later chunk is malformed (an original size that
+    breaks the tile's unfiltered size, tile.cc:305-309; a BWR window size off
+    the tile kernel's shapes; a chunk header pointing past the tile): the
+    tile kernel declines them whole after writing earlier chunks, and the
+    statuses are the oracle's (bytes compared for good tiles only)."""
+    from tests.test_gpu_parity import encode
+    rng = np.random.default_rng(808)
+    vals = [np.concatenate([values(v, 16384, rng, 3 * k + c) for c, v in enumerate(("rand", "active", "ramp"))])
+            for k in range(4)]
+    case = Case("c5_mc_bad", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
+    op, enc = encode(oracle_mod, case)
+    tiles = [e[0].copy() for e in enc]
+    h = _chunk_headers(tiles[1])
+    tiles[1][h[2]:h[2] + 4] = np.frombuffer(np.uint32(65532).tobytes(), dtype=np.uint8)  # orig of chunk 2
+    h = _chunk_headers(tiles[2])
+    tiles[2][h[1] + 4:h[1] + 8] = np.frombuffer(np.uint32(1 << 30).tobytes(), dtype=np.uint8)  # filtered past the tile
+    dp = eng.DevicePipeline(case.serialized, 23, int(Datatype.INT32), 4)
+    refs = [op.unfilter_tile(t, e[2]) for t, e in zip(tiles, enc)]
+    assert refs[0][0] == 0 and refs[3][0] == 0 and refs[1][0] != 0 and refs[2][0] != 0
+    idx = np.arange(MC_TILES) % len(tiles)
+    batch = eng.TileBatch.from_host([tiles[i] for i in idx], [enc[i][2] for i in idx])
+    k0 = ctx.tile_chunks()
+    st = ctx.unfilter(dp, batch)
+    out = batch.outputs_host()
+    for k, i in enumerate(idx):
+        assert int(st[k]) == refs[i][0], f"tile {k}: status {st[k]} oracle {refs[i][0]}"
+        if refs[i][0] == 0:
+            o = int(batch.out_off[k])
+            assert np.array_equal(out[o:o + enc[i][2]], refs[i][1]), f"tile {k}"
+    assert ctx.tile_chunks() - k0 == 3 * sum(1 for i in idx if refs[i][0] == 0)

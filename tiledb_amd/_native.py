@@ -101,6 +101,7 @@ SIGNATURES = {
     "tdbg_dense_read_host": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             ctypes.c_uint64, ctypes.c_uint32, c_i32p, ctypes.c_uint64]),
     "tdbg_context_stream_chunk_stats": (ctypes.c_int, [c_vp, c_u64p]),
+    "tdbg_context_tile_chunk_stats": (ctypes.c_int, [c_vp, c_u64p]),
     "tdbg_dense_copy_fragments_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                        c_vp, c_vp, c_vp]),
     "tdbg_dense_var_offsets_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -34,6 +34,8 @@ NPART = 6  # fused-kernel spec table split (TDBG_NPART; tdbg_host.cpp TDBG_NPART
 UNITS = ([("tdbg_kernels.hip", "tdbg_kernels", []), ("tdbg_chunkdir.hip", "tdbg_chunkdir", []), ("tdbg_host.cpp", "tdbg_host", []),
           ("tdbg_forward.hip", "tdbg_forward", []),
           ("tdbg_c5tile.hip", "tdbg_c5tile", []),
+          # the C5 tile kernel's multi-chunk variant (TDBG_MULTI_CHUNK launches)
+          ("tdbg_c5tile.hip", "tdbg_c5tile_mc", ["-DTDBG_C5T_MC_UNIT", "-mllvm", "-disable-machine-licm"]),
           ("tdbg_c2tile.hip", "tdbg_c2tile", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small", []),
           ("tdbg_stream_small.hip", "tdbg_stream_small_512", ["-DTDBG_SMALL_NT=512"]),

@@ -74,6 +74,12 @@ struct Lds {
   uint2 TAB[TABN];  // {image offset of the window's data | kind << 20, window minimum}
   uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1, Lb, values
   uint32_t red[16][2];  // coded tiles: each wave's DD aggregate (A, B)
+  // multi-chunk tiles (MC): the chunk loop's state, kept here rather than in
+  // registers through the loop (its body is the whole decoder): the next
+  // chunk's header byte in the tile, its output byte, its header [orig,
+  // filtered, md], the chunk index, the chunk count, any chunk raw, the
+  // tile's input and output pointers (lo, hi)
+  uint32_t mcs[12];
 };
 
 // the tile's shape is one this kernel decodes (descriptor checks only)
@@ -81,6 +87,13 @@ struct Lds {
 __device__ __forceinline__ bool takes(const KParams& kp, const Desc& d) {
   return !(kp.flags & TDBG_TILE_OFFSETS) && d.os >= 64 && d.os <= OUTB && (d.os & 3) == 0 &&
          (((uintptr_t)d.out) & 3) == 0 && d.fs <= IMG_CAP;
+}
+
+// a tile of several chunks this kernel may decode in tile mode (its chunks
+// are checked one by one as they come)
+__device__ __forceinline__ bool mc_tile(const KParams& kp, const Desc& d) {
+  return !(kp.flags & TDBG_TILE_OFFSETS) && d.os > OUTB && d.os < (1ull << 32) && d.fs < (1ull << 32) &&
+         (d.os & 3) == 0 && (((uintptr_t)d.out) & 3) == 0 && d.fs >= 8 + 2 * 12;
 }
 
 __device__ __forceinline__ void decline(const KParams& kp, uint64_t t) {
@@ -564,11 +577,14 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
 // (DMA, barriers, constant stores), 2 parse but no decode, 3 no stores,
 // 4 every wave on the one-read path, 5 no 8-bit combine, 6 two halves of 8
 // one-read ranges
-template <bool SGN, int ABL>
+// MC: the multi-chunk variant (launches flagged TDBG_MULTI_CHUNK): tiles of
+// several chunks are decoded chunk after chunk by their workgroup; without
+// it they are declined (the fused kernel takes them).
+template <bool SGN, int ABL, bool MC>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   __shared__ Lds L;
-  const uint32_t w = wave_(), l = lane_();
+  const uint32_t w0 = wave_(), l0 = lane_();
   // diagnostics (KParams::prof, TDBG_PROF=1): shader clocks of workgroups
   // < 1024 (slots 8.. of the profile buffer's rows; the fused kernel, which runs
   // next, writes 0..7): 0 DMA wait, 1 parse, 2 range setup,
@@ -576,8 +592,11 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   uint64_t* const prof = kp.prof && blockIdx.x < 1024 ? kp.prof + (uint64_t)blockIdx.x * TDBG_PROF_PHASES + 8 : nullptr;
   const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   // this workgroup's work item: the XCD-contiguous deal of [base, base + cnt)
+  // (chunk mode: cnt is the directory's capacity, the records are [0, device
+  // count), so workgroups take them round-robin, which spreads the real ones
+  // over every XCD however few they are -- ADVICE r5)
   const uint32_t n8 = (cnt + 7) >> 3;
-  const uint32_t j = (blockIdx.x & 7) * n8 + (blockIdx.x >> 3);
+  const uint32_t j = kp.chunks ? blockIdx.x : (blockIdx.x & 7) * n8 + (blockIdx.x >> 3);
   if (j >= cnt) return;
   const uint64_t t = (uint64_t)base + j;
   if (t >= work_items(kp)) return;
@@ -588,126 +607,197 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   // is not passed here)
   if (kp.fbq && blockIdx.x == 0 && threadIdx.x == 0) kp.fbq[0] = 0;
   const Desc d = load_desc(kp, t);
-  if (!takes(kp, d)) {
+  // A tile of several chunks (tile mode; TileDB splits tiles over 64 KiB
+  // into chunks of at most 64 KiB, tile.cc:87-100): this workgroup decodes
+  // its chunks one after the other (FilterPipeline::run_reverse's loop over
+  // chunks, filter_pipeline.cc:439-517).  The tile's chunk count and chunk
+  // 0's header come from one load; each later chunk's 12-byte header rides
+  // at the end of the previous chunk's image DMA.
+  const bool mc = MC && !takes(kp, d) && !chunked && mc_tile(kp, d);
+  if (!takes(kp, d) && !mc) {
     decline(kp, t);
     return;
   }
-  // The image's aligned cover by LDS-DMA.  Wave 0 first moves the prefix
-  // (units [0, PFX): tile and chunk headers, every window header, the frame
-  // and the DD headers -- all the parse reads) and parses as soon as that
-  // has landed, while the rest of the image (units PFX + 64 (w + 16 i) + l,
-  // every wave) is still in flight; one barrier then publishes the landed
-  // image and the parse.
-  {
-    const uint64_t a0 = (uint64_t)d.in & ~15ull;
-    const uint32_t nu = (uint32_t)((((uint64_t)d.in & 15) + d.fs + 15) >> 4);
-    if (w == 0) {
-#pragma unroll
-      for (uint32_t k = 0; k < PFX / 64; k++)
-        if (64 * k < nu && 64 * k + l < nu) dma16(a0 + 16ull * (64 * k + l), lds_addr(L.IMG) + 1024 * k);
-    }
-    uint32_t after = 0;  // DMA instructions this wave issues after the prefix
-#pragma unroll
-    for (uint32_t i = 0; i < (IMGU - PFX + NT - 1) / NT; i++) {
-      const uint32_t u0 = PFX + 64 * (w + 16 * i);
-      if (u0 < nu) {
-        after++;
-        if (u0 + l < nu) dma16(a0 + 16ull * (u0 + l), lds_addr(L.IMG) + 16 * u0);
-      }
-    }
-    if (w == 0 && ABL != 1) {
-      // (vmcnt counts in issue order: the prefix has landed when at most
-      // `after` of this wave's DMA instructions are left)
-      switch (__builtin_amdgcn_readfirstlane(after)) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-      }
-      // (the parse is the one serial step of a tile: it issues first on its
-      // SIMD, ahead of the other workgroup's waves)
-      __builtin_amdgcn_s_setprio(3);
-      parse<SGN>(L, d, l, chunked);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  const uint64_t c1 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  const uint64_t c2 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
-    decline(kp, t);
-    return;
-  }
-  const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
-  const uint32_t b = (uint32_t)((uintptr_t)d.in & 15);
-  const uint32_t cb = __builtin_amdgcn_readfirstlane(L.hd[3]);
-  const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
-  const uint32_t nv = __builtin_amdgcn_readfirstlane(L.hd[7]);
-  if (cb != 0) {
-    // coded DoubleDelta: one instantiation per code width
-    switch (cb) {
-#define TDBG_CB(c) \
-  case c: coded_tile<c, SGN, ABL>(L, d, b, wsh - 2, wlast, w, l, nv, prof); break;
-      TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
-      TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
-      TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
-      TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
-      TDBG_CB(31)
-#undef TDBG_CB
-      default: break;
-    }
-    if (prof && threadIdx.x == 0) {
-      prof[0] = c1 - c0;
-      prof[1] = c2 - c1;
+  if (mc) {
+    // (uniform values: made scalar, so that nothing of the loop below is
+    // taken for a per-lane value)
+    const uint64_t n = ldn(d.in, 8);
+    const uint32_t nlo = __builtin_amdgcn_readfirstlane((uint32_t)n), nhi = __builtin_amdgcn_readfirstlane((uint32_t)(n >> 32));
+    if (nhi != 0 || nlo < 2 || nlo > (d.fs - 8) / 12) {
+      decline(kp, t);
+      return;
     }
     if (threadIdx.x == 0) {
-      if (kp.status && !chunked) kp.status[t] = TDBG_OK;
-      if (kp.stats) {
-        uint64_t* s = kp.stats + TDBG_STAT_STRIDE * (1 + (blockIdx.x & 63));
-        if (chunked) {
-          atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_CHUNKS], 1ull);
-        } else {
-          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
-          atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)d.os);
-          atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
+      L.mcs[0] = 8;  // chunk 0's header follows the u64 chunk count
+      L.mcs[1] = 0;
+      L.mcs[2] = (uint32_t)ldn(d.in + 8, 4);
+      L.mcs[3] = (uint32_t)ldn(d.in + 12, 4);
+      L.mcs[4] = (uint32_t)ldn(d.in + 16, 4);
+      L.mcs[5] = 0;
+      L.mcs[6] = nlo;
+      L.mcs[7] = 0;
+      L.mcs[8] = (uint32_t)(uintptr_t)d.in;
+      L.mcs[9] = (uint32_t)((uintptr_t)d.in >> 32);
+      L.mcs[10] = (uint32_t)(uintptr_t)d.out;
+      L.mcs[11] = (uint32_t)((uintptr_t)d.out >> 32);
+    }
+    lds_barrier();
+  }
+  bool any_raw = false;
+  for (uint32_t k = 0;; k++) {
+    // (the lane index made opaque per chunk: nothing per-lane is computed
+    // once before the loop and held in registers through it)
+    uint32_t l = l0, w = w0, img = lds_addr(L.IMG);
+    if (MC) {
+      l = lane_();
+      asm volatile("" : "+s"(w), "+s"(img));  // (the same for the wave and the LDS addresses derived from them)
+    }
+    Desc dk = d;
+    uint32_t extra = 0;  // bytes DMA'd past the image: the next chunk's header
+    if (mc) {
+      auto S = [&](int i) -> uint32_t { return __builtin_amdgcn_readfirstlane(L.mcs[i]); };
+      const uint32_t cur = S(0), out_off = S(1), ho = S(2), hf = S(3), hm = S(4), kk = S(5), nch = S(6);
+      const uint64_t tin = ((uint64_t)S(9) << 32) | S(8), tout = ((uint64_t)S(11) << 32) | S(10);
+      const bool last = kk + 1 == nch;
+      const uint64_t cfs = 12ull + hm + hf;
+      extra = last ? 0u : 12u;
+      // the chunk is one this kernel decodes, lies inside the tile, and (the
+      // last one) completes the tile's unfiltered size (tile.cc:305-309)
+      const bool ok = (uint64_t)cur + cfs + extra <= d.fs && ho >= 64 && ho <= OUTB && (ho & 3) == 0 &&
+                      cfs + extra <= IMG_CAP && (uint64_t)out_off + ho <= d.os &&
+                      (!last || (uint64_t)out_off + ho == d.os);
+      if (!ok) {
+        decline(kp, t);
+        return;
+      }
+      dk.fs = cfs;
+      dk.os = ho;
+      dk.in = (const uint8_t*)(tin + cur);
+      dk.out = (uint8_t*)(tout + out_off);
+    }
+    uint64_t* const pf = mc ? nullptr : prof;
+    // The image's aligned cover by LDS-DMA.  Wave 0 first moves the prefix
+    // (units [0, PFX): tile and chunk headers, every window header, the frame
+    // and the DD headers -- all the parse reads) and parses as soon as that
+    // has landed, while the rest of the image (units PFX + 64 (w + 16 i) + l,
+    // every wave) is still in flight; one barrier then publishes the landed
+    // image and the parse.  (Multi-chunk: the previous chunk's stores are
+    // older than this DMA in each wave's in-order vmcnt, so the counted waits
+    // below also wait for them.)
+    {
+      const uint64_t a0 = (uint64_t)dk.in & ~15ull;
+      const uint32_t nu = (uint32_t)((((uint64_t)dk.in & 15) + dk.fs + extra + 15) >> 4);
+      if (w == 0) {
+#pragma unroll
+        for (uint32_t q = 0; q < PFX / 64; q++)
+          if (64 * q < nu && 64 * q + l < nu) dma16(a0 + 16ull * (64 * q + l), img + 1024 * q);
+      }
+      uint32_t after = 0;  // DMA instructions this wave issues after the prefix
+#pragma unroll
+      for (uint32_t i = 0; i < (IMGU - PFX + NT - 1) / NT; i++) {
+        const uint32_t u0 = PFX + 64 * (w + 16 * i);
+        if (u0 < nu) {
+          after++;
+          if (u0 + l < nu) dma16(a0 + 16ull * (u0 + l), img + 16 * u0);
         }
       }
+      if (w == 0 && ABL != 1) {
+        // (vmcnt counts in issue order: the prefix has landed when at most
+        // `after` of this wave's DMA instructions are left)
+        switch (__builtin_amdgcn_readfirstlane(after)) {
+          case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+          case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+          case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+          case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+          default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        }
+        // (the parse is the one serial step of a tile: it issues first on its
+        // SIMD, ahead of the other workgroup's waves)
+        __builtin_amdgcn_s_setprio(3);
+        parse<SGN>(L, dk, l, chunked || mc);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
-    return;
-  }
-  const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh, wlast, nv);
-  uint8_t* const o = d.out + 16u * (64 * w + l);
-  const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
-  // All 16 ranges' reads first, then the decode and one store per round.
-  // Raw and 8-bit ranges read one dword (the decoder picked by a select).
-  // The few general ranges (a wave of a ramp tile on a plane boundary) take
-  // the per-element decoder under a wave-uniform branch that holds no LDS
-  // access, so the reads stay in flight together (8 at a time in such waves,
-  // for registers).  (Measured, not kept: the general rounds first, one at a
-  // time, then all 16 one-read ranges together -- ramp -0.9 %, rand -1.1 %
-  // on one box, profiles/r06/ab_general_first.txt.)
-  if (g.gen == 0 || ABL == 4) {
-    decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
-  } else if (ABL == 6) {
-    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
-    decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv);
-  } else {
-    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0, nv);
-    decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2, nv);
-  }
-  if (prof && l == 0) {
-    const uint64_t c4 = __builtin_amdgcn_s_memtime();
-    if (w == 0) {
-      prof[0] = c1 - c0;
-      prof[1] = c2 - c1;
-      prof[2] = c3 - c2;
-      prof[3] = c4 - c3;
-      prof[6] = c4 - c0;
+    const uint64_t c1 = pf ? __builtin_amdgcn_s_memtime() : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    const uint64_t c2 = pf ? __builtin_amdgcn_s_memtime() : 0;
+    if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
+      decline(kp, t);
+      return;
     }
-    if (w == 1) prof[4] = c4 - c3;
-    if (w == 15) prof[5] = c4 - c3;
+    const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
+    const uint32_t b = (uint32_t)((uintptr_t)dk.in & 15);
+    const uint32_t cb = __builtin_amdgcn_readfirstlane(L.hd[3]);
+    const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
+    const uint32_t nv = __builtin_amdgcn_readfirstlane(L.hd[7]);
+    if (mc && threadIdx.x == 0) {
+      // the loop state for the next chunk: its header (DMA'd behind this
+      // image; read before the end-of-chunk barrier lets the next DMA land)
+      const uint32_t hb = b + (uint32_t)dk.fs;
+      if (extra) {
+        L.mcs[2] = rd32(L.IMG, hb);
+        L.mcs[3] = rd32(L.IMG, hb + 4);
+        L.mcs[4] = rd32(L.IMG, hb + 8);
+      }
+      L.mcs[0] += (uint32_t)dk.fs;
+      L.mcs[1] += (uint32_t)dk.os;
+      L.mcs[5] += 1;
+    }
+    if (cb != 0) {
+      // coded DoubleDelta: one instantiation per code width
+      switch (cb) {
+#define TDBG_CB(c) \
+  case c: coded_tile<c, SGN, ABL>(L, dk, b, wsh - 2, wlast, w, l, nv, pf); break;
+        TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
+        TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
+        TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
+        TDBG_CB(24) TDBG_CB(25) TDBG_CB(26) TDBG_CB(27) TDBG_CB(28) TDBG_CB(29) TDBG_CB(30)
+        TDBG_CB(31)
+#undef TDBG_CB
+        default: break;
+      }
+      if (pf && threadIdx.x == 0) {
+        pf[0] = c1 - c0;
+        pf[1] = c2 - c1;
+      }
+    } else {
+      any_raw = true;
+      const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh, wlast, nv);
+      uint8_t* const o = dk.out + 16u * (64 * w + l);
+      const uint64_t c3 = pf ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
+      // All 16 ranges' reads first, then the decode and one store per round.
+      // Raw and 8-bit ranges read one dword (the decoder picked by a select).
+      // The few general ranges (a wave of a ramp tile on a plane boundary)
+      // take the per-element decoder under a wave-uniform branch that holds
+      // no LDS access, so the reads stay in flight together (8 at a time in
+      // such waves, for registers).  (Measured, not kept: the general rounds
+      // first, one at a time, then all 16 one-read ranges together -- ramp
+      // -0.9 %, rand -1.1 % on one box, profiles/r06/ab_general_first.txt.)
+      if (g.gen == 0 || ABL == 4) {
+        decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
+      } else if (ABL == 6) {
+        decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
+        decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv);
+      } else {
+        decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0, nv);
+        decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2, nv);
+      }
+      if (pf && l == 0) {
+        const uint64_t c4 = __builtin_amdgcn_s_memtime();
+        if (w == 0) {
+          pf[0] = c1 - c0;
+          pf[1] = c2 - c1;
+          pf[2] = c3 - c2;
+          pf[3] = c4 - c3;
+          pf[6] = c4 - c0;
+        }
+        if (w == 1) pf[4] = c4 - c3;
+        if (w == 15) pf[5] = c4 - c3;
+      }
+    }
+    if (!mc || extra == 0) break;  // (the last chunk DMA'd no next header)
+    lds_barrier();  // every wave is done with this chunk's image, table and headers
   }
   if (threadIdx.x == 0) {
     if (kp.status && !chunked) kp.status[t] = TDBG_OK;
@@ -722,7 +812,8 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_TILES], 1ull);
         atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)d.os);
         atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
-        atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_RAW_TILES], 1ull);
+        if (any_raw && !mc) atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_RAW_TILES], 1ull);
+        if (mc) atomicAdd((unsigned long long*)&s[TDBG_STAT_TILE_CHUNKS], (unsigned long long)L.mcs[6]);
       }
     }
   }
@@ -734,21 +825,9 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
 // one workgroup per work item (kp->ntiles of them, or in chunk mode the
 // directory's capacity: items past the device count exit at once); launches
 // of at most GRID_CAP items
-extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s) {
+template <typename K>
+static hipError_t c5tile_grid(K k, const tdbg::KParams* kp, hipStream_t s) {
   using namespace tdbg::c5t;
-#ifdef TDBG_EXPERIMENTS
-  static const int abl = tdbg_hook("TDBG_C5T_ABL") ? atoi(tdbg_hook("TDBG_C5T_ABL")) : 0;  // experiments
-  auto k = sgn ? (abl == 1   ? unfilter_c5tile_kernel<true, 1>
-                  : abl == 2 ? unfilter_c5tile_kernel<true, 2>
-                  : abl == 3 ? unfilter_c5tile_kernel<true, 3>
-                  : abl == 4 ? unfilter_c5tile_kernel<true, 4>
-                  : abl == 5 ? unfilter_c5tile_kernel<true, 5>
-                  : abl == 6 ? unfilter_c5tile_kernel<true, 6>
-                             : unfilter_c5tile_kernel<true, 0>)
-               : unfilter_c5tile_kernel<false, 0>;
-#else
-  auto k = sgn ? unfilter_c5tile_kernel<true, 0> : unfilter_c5tile_kernel<false, 0>;
-#endif
   for (uint64_t base = 0; base < kp->ntiles; base += GRID_CAP) {
     const uint32_t cnt = (uint32_t)std::min<uint64_t>(kp->ntiles - base, GRID_CAP);
     const uint32_t grid = 8 * ((cnt + 7) / 8);
@@ -758,3 +837,36 @@ extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipSt
   }
   return hipSuccess;
 }
+
+#ifdef TDBG_C5T_MC_UNIT
+// The multi-chunk variant is its own translation unit, compiled with
+// -mllvm -disable-machine-licm (tiledb_amd/build.py): its chunk loop holds
+// the whole decoder, and loop-invariant code hoisted out of it (LDS
+// addresses, kernel-argument tests) outgrew the 64 VGPRs of 8 waves per SIMD
+// and spilled to scratch, which the counted vmcnt waits cannot allow.
+extern "C" hipError_t tdbg_launch_c5tile_mc(const tdbg::KParams* kp, int sgn, hipStream_t s) {
+  using namespace tdbg::c5t;
+  return c5tile_grid(sgn ? unfilter_c5tile_kernel<true, 0, true> : unfilter_c5tile_kernel<false, 0, true>, kp, s);
+}
+#else
+extern "C" hipError_t tdbg_launch_c5tile_mc(const tdbg::KParams* kp, int sgn, hipStream_t s);
+
+extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, int mc, hipStream_t s) {
+  using namespace tdbg::c5t;
+  if (mc) return tdbg_launch_c5tile_mc(kp, sgn, s);
+#ifdef TDBG_EXPERIMENTS
+  static const int abl = tdbg_hook("TDBG_C5T_ABL") ? atoi(tdbg_hook("TDBG_C5T_ABL")) : 0;  // experiments
+  auto k = sgn ? (abl == 1   ? unfilter_c5tile_kernel<true, 1, false>
+                  : abl == 2 ? unfilter_c5tile_kernel<true, 2, false>
+                  : abl == 3 ? unfilter_c5tile_kernel<true, 3, false>
+                  : abl == 4 ? unfilter_c5tile_kernel<true, 4, false>
+                  : abl == 5 ? unfilter_c5tile_kernel<true, 5, false>
+                  : abl == 6 ? unfilter_c5tile_kernel<true, 6, false>
+                             : unfilter_c5tile_kernel<true, 0, false>)
+               : unfilter_c5tile_kernel<false, 0, false>;
+#else
+  auto k = sgn ? unfilter_c5tile_kernel<true, 0, false> : unfilter_c5tile_kernel<false, 0, false>;
+#endif
+  return c5tile_grid(k, kp, s);
+}
+#endif

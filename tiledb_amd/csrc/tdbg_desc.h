@@ -60,7 +60,8 @@ enum tdbg_stat_slot : uint32_t {
   TDBG_STAT_STREAM_RAW_TILES = 6,  // of those: the raw-DoubleDelta kernel's (tdbg_stream_raw.hip)
   TDBG_STAT_FWD_STREAM_TILES = 7,  // forward: tiles the LDS-resident C5 kernel filtered (tdbg_forward_stream.hip)
   TDBG_STAT_STREAM_CHUNKS = 8,  // chunk-parallel launches: chunks the streaming kernels took
-  TDBG_STAT_N = 9
+  TDBG_STAT_TILE_CHUNKS = 9,    // tile mode: chunks of multi-chunk tiles the C5 tile kernel took
+  TDBG_STAT_N = 10
 };
 // The counters live in slots of TDBG_STAT_STRIDE u64 (one 128-B line each):
 // slot 0 takes the persistent kernels' one add per workgroup, slots 1..64 the

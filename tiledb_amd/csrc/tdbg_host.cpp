@@ -70,7 +70,7 @@ extern "C" uint32_t tdbg_stream_grid(int cus);
 extern "C" hipError_t tdbg_launch_stream_raw(const tdbg::KParams* kp, uint32_t grid, int sgn, hipStream_t s);
 extern "C" uint32_t tdbg_stream_raw_grid(int cus);
 #endif
-extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, hipStream_t s);
+extern "C" hipError_t tdbg_launch_c5tile(const tdbg::KParams* kp, int sgn, int mc, hipStream_t s);
 extern "C" hipError_t tdbg_launch_c2tile(const tdbg::KParams* kp, int mode, int sgn, hipStream_t s);
 extern "C" hipError_t tdbg_launch_stream_small(const tdbg::KParams* kp, uint32_t grid, int mode, int sgn,
                                                hipStream_t s);
@@ -702,8 +702,14 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
   // would then bound the parallelism).  The directory pass runs first on
   // the same stream; its records feed the fused kernel.
   static const bool tile_mode = tdbg_hook("TDBG_DEBUG_TILE_MODE") != nullptr;  // ablation: no auto chunk mode
+  // (TDBG_MULTI_CHUNK: the caller has tiles of several chunks; a launch of
+  // fewer than two tiles per CU -- two workgroups of the C5 tile kernel fit
+  // a CU -- then spreads their chunks through the directory, a bigger one
+  // runs tile mode with the tile kernel's multi-chunk variant)
   const bool chunked = queued && !d_list &&
-                       ((flags & TDBG_CHUNK_PARALLEL) || (!tile_mode && ntiles < (uint64_t)c->cus));
+                       ((flags & TDBG_CHUNK_PARALLEL) ||
+                        (!tile_mode && (ntiles < (uint64_t)c->cus ||
+                                        ((flags & TDBG_MULTI_CHUNK) && ntiles < 2 * (uint64_t)c->cus))));
   // [BYTESHUFFLE] on 4-byte values (C1): the unit-parallel streaming kernel
   // (tdbg_stream_shuffle.hip) splits every one-chunk 64 KiB tile over 16
   // workgroups itself; batches of fewer tiles than CUs (e.g. a few
@@ -846,7 +852,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       } else
 #endif
       if (!skip_fused) {
-        e = tdbg_launch_c5tile(&ks, sgn, stream);
+        e = tdbg_launch_c5tile(&ks, sgn, 0, stream);
       }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
@@ -892,7 +898,7 @@ static int launch(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
       } else
 #endif
       if (!skip_fused) {
-        e = tdbg_launch_c5tile(&ks, sgn, stream);
+        e = tdbg_launch_c5tile(&ks, sgn, (flags & TDBG_MULTI_CHUNK) ? 1 : 0, stream);
       }
       if (e != hipSuccess) return fail(TDBG_E_DEVICE, std::string("raw stream kernel launch: ") + hipGetErrorString(e));
     }
@@ -1409,6 +1415,15 @@ int tdbg_context_stream_chunk_stats(const tdbg_context* c, uint64_t* chunks) {
   return TDBG_OK;
 }
 
+int tdbg_context_tile_chunk_stats(const tdbg_context* c, uint64_t* chunks) {
+  if (!c) return fail(TDBG_E_ARG, "null context");
+  uint64_t h[TDBG_STAT_N];
+  int rc = read_stats(c, h);
+  if (rc) return rc;
+  if (chunks) *chunks = h[TDBG_STAT_TILE_CHUNKS];
+  return TDBG_OK;
+}
+
 int tdbg_context_forward_stream_stats(const tdbg_context* c, uint64_t* tiles) {
   if (!c) return fail(TDBG_E_ARG, "null context");
   uint64_t h[TDBG_STAT_N];
@@ -1564,6 +1579,15 @@ static int copy_ranges(hipStream_t st, uint64_t lo, uint64_t hi, const uint8_t* 
   return TDBG_OK;
 }
 
+// TDBG_MULTI_CHUNK when a tile of the call (host-known sizes) is larger than
+// the pipeline's chunks (tile.cc:87-100)
+static uint32_t multi_chunk_flag(const tdbg_pipeline* p, uint64_t ntiles, const uint64_t* out_size) {
+  const uint64_t mc = p->max_chunk_size ? p->max_chunk_size : 65536;
+  for (uint64_t i = 0; i < ntiles; i++)
+    if (out_size[i] > mc) return TDBG_MULTI_CHUNK;
+  return 0;
+}
+
 static int unfilter_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntiles,
                          const uint8_t* const* in, const uint64_t* in_size,
                          uint8_t* const* out, const uint64_t* out_size, const uint64_t* var_size,
@@ -1577,6 +1601,7 @@ static int unfilter_host(tdbg_context* c, const tdbg_pipeline* p, uint64_t ntile
   const bool cin = (flags & TDBG_HOST_CONTIGUOUS_INPUT) != 0;
   const bool cout = (flags & TDBG_HOST_CONTIGUOUS_OUTPUT) != 0;
   flags &= ~(TDBG_HOST_CONTIGUOUS_INPUT | TDBG_HOST_CONTIGUOUS_OUTPUT);
+  flags |= multi_chunk_flag(p, ntiles, out_size);
   if (!c->cstream) HIP_OK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
   if (!c->hstream) HIP_OK(hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking));
   if (!c->dstream) HIP_OK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));

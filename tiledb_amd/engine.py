@@ -24,6 +24,7 @@ TILE_OFFSETS = 0x1  # TDBG_TILE_OFFSETS
 HOST_CONTIGUOUS_INPUT = 0x2   # TDBG_HOST_CONTIGUOUS_INPUT
 HOST_CONTIGUOUS_OUTPUT = 0x4  # TDBG_HOST_CONTIGUOUS_OUTPUT
 CHUNK_PARALLEL = 0x8  # TDBG_CHUNK_PARALLEL
+MULTI_CHUNK = 0x10  # TDBG_MULTI_CHUNK
 E_NOT_RUN = 19  # TDBG_E_NOT_RUN
 # call-level failures (not a tile's status): raised even when tiles carry statuses
 CALL_ERRORS = (1, 10, 14, 15, 17)  # TDBG_E_ARG, _UNSUPPORTED, _DEVICE, _DESCRIPTOR, _INTERNAL
@@ -262,28 +263,35 @@ class Context:
 
     @staticmethod
     def auto_chunk_parallel(dp: DevicePipeline, batch: TileBatch) -> bool:
-        """TDBG_CHUNK_PARALLEL when a tile holds more than one chunk (an
-        unfiltered size above the pipeline's max chunk size,
-        FilterPipeline::serialize's first u32; tile.cc:87-100): the chunk
-        directory then spreads the chunks over the GPU, where a tile-serial
-        launch decodes a tile's chunks one after another in one workgroup
-        (C5, 512 tiles of 4 MiB: 0.34 -> 0.46 of 8 TB/s, profiles/r05/c5big_ab.txt)."""
+        """Whether a tile holds more than one chunk (an unfiltered size above
+        the pipeline's max chunk size, FilterPipeline::serialize's first u32;
+        tile.cc:87-100): such launches carry TDBG_MULTI_CHUNK, and the engine
+        then runs the C5 tile kernel's multi-chunk variant when the launch
+        has tiles enough to fill the GPU, or the device chunk directory
+        (chunk-parallel) when it has fewer."""
         if batch.ntiles == 0 or len(dp.serialized) < 4:
             return False
         mc = int(np.frombuffer(dp.serialized[:4], dtype="<u4")[0]) or 65536
         return bool(int(batch.out_size.max()) > mc)
 
+    def _launch_flags(self, dp, batch, offsets_tiles, chunk_parallel) -> int:
+        """chunk_parallel: None = TDBG_MULTI_CHUNK when auto_chunk_parallel
+        (the engine picks tile or chunk mode); True = TDBG_CHUNK_PARALLEL;
+        False = neither."""
+        f = TILE_OFFSETS if offsets_tiles else 0
+        if chunk_parallel is None:
+            return f | (MULTI_CHUNK if self.auto_chunk_parallel(dp, batch) else 0)
+        return f | (CHUNK_PARALLEL if chunk_parallel else 0)
+
     def unfilter(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
                  stream=None, chunk_parallel=None) -> np.ndarray:
         """Synchronous unfilter; returns the per-tile status array.
-        chunk_parallel: None = auto_chunk_parallel."""
-        if chunk_parallel is None:
-            chunk_parallel = self.auto_chunk_parallel(dp, batch)
+        chunk_parallel: see _launch_flags."""
         st = np.zeros(max(batch.ntiles, 1), dtype=np.int32)
         pin, psz, pout, posz = batch.ptrs()
         rc = lib.tdbg_unfilter_tiles_sync(
             self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
-            (TILE_OFFSETS if offsets_tiles else 0) | (CHUNK_PARALLEL if chunk_parallel else 0),
+            self._launch_flags(dp, batch, offsets_tiles, chunk_parallel),
             st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self._stream(stream))
         if rc and not st[: batch.ntiles].any():
             _check(rc, "tdbg_unfilter_tiles_sync")
@@ -291,12 +299,10 @@ class Context:
 
     def unfilter_async(self, dp: DevicePipeline, batch: TileBatch, offsets_tiles: bool = False,
                        stream=None, chunk_parallel=None) -> None:
-        if chunk_parallel is None:
-            chunk_parallel = self.auto_chunk_parallel(dp, batch)
         pin, psz, pout, posz = batch.ptrs()
         _check(lib.tdbg_unfilter_tiles_async(
             self.h, dp.h, batch.ntiles, pin, psz, pout, posz,
-            (TILE_OFFSETS if offsets_tiles else 0) | (CHUNK_PARALLEL if chunk_parallel else 0),
+            self._launch_flags(dp, batch, offsets_tiles, chunk_parallel),
             batch.d_status.data_ptr(), self._stream(stream)), "tdbg_unfilter_tiles_async")
 
     def filter_batch(self, dp: DevicePipeline, tiles: Sequence, max_chunk: int = 0) -> "FilterBatch":
@@ -343,6 +349,15 @@ class Context:
         """Tiles the LDS-resident C5 forward kernel filtered, cumulative (synchronizes)."""
         n = ctypes.c_uint64()
         _check(lib.tdbg_context_forward_stream_stats(self.h, ctypes.byref(n)), "tdbg_context_forward_stream_stats")
+        return int(n.value)
+
+    def tile_chunks(self):
+        """Chunks of multi-chunk tiles the C5 tile kernel took in tile mode
+        (TDBG_MULTI_CHUNK launches), cumulative."""
+        if "tdbg_context_tile_chunk_stats" in _native.MISSING:  # (an older TDBG_LIB build)
+            return 0
+        n = ctypes.c_uint64()
+        _check(lib.tdbg_context_tile_chunk_stats(self.h, ctypes.byref(n)), "tdbg_context_tile_chunk_stats")
         return int(n.value)
 
     def stream_chunks(self):
