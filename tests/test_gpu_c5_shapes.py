@@ -268,7 +268,9 @@ def test_c5_multichunk_tile_mode(eng, ctx, oracle_mod, align):
         vals.append(np.concatenate(parts))
     case = Case("c5_mc", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
     want_c, took_c, want_t, took_t, fb = _mc_tile_mode(eng, ctx, oracle_mod, case, align=align)
-    assert fb == 0
+    # (the fused kernel passes the 2-value chunk's tiles on to the general
+    # interpreter: only tiles the tile kernel declined may fall back)
+    assert fb <= MC_TILES - want_t
     assert want_t < MC_TILES and want_t > MC_TILES // 2  # (the 2-value last chunk's tiles are declined)
     assert took_c == want_c, f"took {took_c} chunks, expected {want_c}"
     assert took_t == want_t

@@ -75,11 +75,12 @@ struct Lds {
   uint32_t hd[8];   // verdict, log2(window bytes), nwin - 1, code width (0: raw DD), x0, x1, Lb, values
   uint32_t red[16][2];  // coded tiles: each wave's DD aggregate (A, B)
   // multi-chunk tiles (MC): the chunk loop's state, kept here rather than in
-  // registers through the loop (its body is the whole decoder): the next
-  // chunk's header byte in the tile, its output byte, its header [orig,
-  // filtered, md], the chunk index, the chunk count, any chunk raw, the
-  // tile's input and output pointers (lo, hi)
-  uint32_t mcs[12];
+  // registers through the loop (its body is the whole decoder).  Per chunk k
+  // (buffer k & 1, written by thread 0 during chunk k - 1): the chunk's
+  // header byte in the tile, its output byte, its header [orig, filtered,
+  // md]; per tile: the chunk count, the tile's input and output pointers
+  uint32_t mcs[2][5];
+  uint32_t mct[5];
 };
 
 // the tile's shape is one this kernel decodes (descriptor checks only)
@@ -314,9 +315,15 @@ __device__ __forceinline__ void store_unit(uint8_t* p, const v4u& v, uint32_t u,
 }
 
 // NR ranges (NR / 4 rounds from round r0): reads, decode, stores
-template <bool SGN, int ABL, bool GEN, int NR>
+// (hook: called by every wave once all of its reads are issued, before the
+// first store -- the multi-chunk variant's point to issue the next chunk's
+// DMA, tdbg_c5tile's chunk loop)
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <bool SGN, int ABL, bool GEN, int NR, typename Hook = NoHook>
 __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint32_t b, uint32_t w, uint32_t l,
-                                             uint8_t* o, uint32_t r0, uint32_t nv) {
+                                             uint8_t* o, uint32_t r0, uint32_t nv, const Hook& hook = Hook()) {
   uint32_t y[NR];
 #pragma unroll
   for (uint32_t j = 0; j < NR; j++) {
@@ -327,6 +334,7 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
     if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b, Q0 & 3);
     y[j] = (ABL == 1 || ABL == 2) ? l + i : rd32(L.IMG, a);
   }
+  hook();
 #pragma unroll
   for (uint32_t rr = 0; rr < NR / 4; rr++) {
     const uint32_t r = r0 + rr;
@@ -484,9 +492,9 @@ __device__ __forceinline__ uint32_t vslot(uint32_t v) {
 // A coded tile: codes, scans (one barrier publishes the 16 wave totals and
 // frees the image), the fold of each lane's prefix into its values, the
 // values into LDS (second barrier), then byteshuffle^-1 and the stores.
-template <int CB, bool SGN, int ABL>
+template <int CB, bool SGN, int ABL, bool MC, typename Hook>
 __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, uint32_t esh, uint32_t wlast,
-                                           uint32_t w, uint32_t l, uint32_t nv, uint64_t* prof) {
+                                           uint32_t w, uint32_t l, uint32_t nv, uint64_t* prof, const Hook& hook) {
   const uint32_t x0 = __builtin_amdgcn_readfirstlane(L.hd[4]), x1 = __builtin_amdgcn_readfirstlane(L.hd[5]);
   uint32_t xk[16], ae, be;
   const uint64_t c3 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -529,14 +537,30 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
     // value 4096 k + 1024 r + T sits at dword vslot(T) + 4096 k + 1024 r (the
     // swizzle depends only on bits of T): one base, constant offsets
     const uint32_t* const vb = L.IMG + vslot(T);
+    if constexpr (MC) {
+      // (every value read before the hook: the next chunk's DMA may then
+      // land over the value buffer while these stores go out)
+      uint32_t x[16];
 #pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-      uint32_t x[4];
+      for (uint32_t r = 0; r < 4; r++)
 #pragma unroll
-      for (uint32_t k = 0; k < 4; k++) x[k] = vb[4096 * k + 1024 * r];
-      const v4u v = unshuffle4(x);
-      if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
-        __builtin_nontemporal_store((v4a)v, (g_a4*)(o + 16384u * r));
+        for (uint32_t k = 0; k < 4; k++) x[4 * r + k] = vb[4096 * k + 1024 * r];
+      hook();
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t y[4] = {x[4 * r], x[4 * r + 1], x[4 * r + 2], x[4 * r + 3]};
+        __builtin_nontemporal_store((v4a)unshuffle4(y), (g_a4*)(o + 16384u * r));
+      }
+    } else {
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) x[k] = vb[4096 * k + 1024 * r];
+        const v4u v = unshuffle4(x);
+        if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
+          __builtin_nontemporal_store((v4a)v, (g_a4*)(o + 16384u * r));
+      }
     }
   } else {
     // nv values: plane k starts at stream byte nv k, so unit u's plane dword
@@ -628,22 +652,47 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       return;
     }
     if (threadIdx.x == 0) {
-      L.mcs[0] = 8;  // chunk 0's header follows the u64 chunk count
-      L.mcs[1] = 0;
-      L.mcs[2] = (uint32_t)ldn(d.in + 8, 4);
-      L.mcs[3] = (uint32_t)ldn(d.in + 12, 4);
-      L.mcs[4] = (uint32_t)ldn(d.in + 16, 4);
-      L.mcs[5] = 0;
-      L.mcs[6] = nlo;
-      L.mcs[7] = 0;
-      L.mcs[8] = (uint32_t)(uintptr_t)d.in;
-      L.mcs[9] = (uint32_t)((uintptr_t)d.in >> 32);
-      L.mcs[10] = (uint32_t)(uintptr_t)d.out;
-      L.mcs[11] = (uint32_t)((uintptr_t)d.out >> 32);
+      L.mcs[0][0] = 8;  // chunk 0's header follows the u64 chunk count
+      L.mcs[0][1] = 0;
+      L.mcs[0][2] = (uint32_t)ldn(d.in + 8, 4);
+      L.mcs[0][3] = (uint32_t)ldn(d.in + 12, 4);
+      L.mcs[0][4] = (uint32_t)ldn(d.in + 16, 4);
+      L.mct[0] = nlo;
+      L.mct[1] = (uint32_t)(uintptr_t)d.in;
+      L.mct[2] = (uint32_t)((uintptr_t)d.in >> 32);
+      L.mct[3] = (uint32_t)(uintptr_t)d.out;
+      L.mct[4] = (uint32_t)((uintptr_t)d.out >> 32);
     }
     lds_barrier();
   }
   bool any_raw = false;
+  // Multi-chunk tiles, pipelined: once every wave has read a full (64 KiB)
+  // chunk out of LDS, the next chunk's image DMA is issued, before this
+  // chunk's stores, so that its latency overlaps them (gfx950 counts loads
+  // and stores in one in-order vmcnt: a DMA issued after the stores would
+  // wait for them).  `issued`: this chunk's DMA went out in the previous
+  // iteration, `after` its DMA instructions past the prefix, `pend` the
+  // stores this wave issued after it (exact: one per full 16-B unit round).
+  bool issued = false, declined = false;
+  uint32_t after = 0, pend = 0;
+  // (vmcnt wait with a run-time count; counts above 12 cannot occur)
+  auto vm_wait = [](uint32_t n) {
+    switch (__builtin_amdgcn_readfirstlane(n)) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+      case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+  };
   for (uint32_t k = 0;; k++) {
     // (the lane index made opaque per chunk: nothing per-lane is computed
     // once before the loop and held in registers through it)
@@ -652,103 +701,127 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       l = lane_();
       asm volatile("" : "+s"(w), "+s"(img));  // (the same for the wave and the LDS addresses derived from them)
     }
-    Desc dk = d;
-    uint32_t extra = 0;  // bytes DMA'd past the image: the next chunk's header
-    if (mc) {
-      auto S = [&](int i) -> uint32_t { return __builtin_amdgcn_readfirstlane(L.mcs[i]); };
-      const uint32_t cur = S(0), out_off = S(1), ho = S(2), hf = S(3), hm = S(4), kk = S(5), nch = S(6);
-      const uint64_t tin = ((uint64_t)S(9) << 32) | S(8), tout = ((uint64_t)S(11) << 32) | S(10);
-      const bool last = kk + 1 == nch;
-      const uint64_t cfs = 12ull + hm + hf;
-      extra = last ? 0u : 12u;
-      // the chunk is one this kernel decodes, lies inside the tile, and (the
-      // last one) completes the tile's unfiltered size (tile.cc:305-309)
-      const bool ok = (uint64_t)cur + cfs + extra <= d.fs && ho >= 64 && ho <= OUTB && (ho & 3) == 0 &&
-                      cfs + extra <= IMG_CAP && (uint64_t)out_off + ho <= d.os &&
-                      (!last || (uint64_t)out_off + ho == d.os);
-      if (!ok) {
-        decline(kp, t);
-        return;
-      }
-      dk.fs = cfs;
-      dk.os = ho;
-      dk.in = (const uint8_t*)(tin + cur);
-      dk.out = (uint8_t*)(tout + out_off);
-    }
-    uint64_t* const pf = mc ? nullptr : prof;
-    // The image's aligned cover by LDS-DMA.  Wave 0 first moves the prefix
+    // The image's aligned cover by LDS-DMA.  Wave 0 moves the prefix first
     // (units [0, PFX): tile and chunk headers, every window header, the frame
-    // and the DD headers -- all the parse reads) and parses as soon as that
-    // has landed, while the rest of the image (units PFX + 64 (w + 16 i) + l,
-    // every wave) is still in flight; one barrier then publishes the landed
-    // image and the parse.  (Multi-chunk: the previous chunk's stores are
-    // older than this DMA in each wave's in-order vmcnt, so the counted waits
-    // below also wait for them.)
-    {
-      const uint64_t a0 = (uint64_t)dk.in & ~15ull;
-      const uint32_t nu = (uint32_t)((((uint64_t)dk.in & 15) + dk.fs + extra + 15) >> 4);
+    // and the DD headers -- all the parse reads); the rest of the image
+    // (units PFX + 64 (w + 16 i) + l) goes out from every wave.  Returns the
+    // DMA instructions this wave issued after the prefix.
+    auto issue_dma = [&](const Desc& q, uint32_t ex) -> uint32_t {
+      const uint64_t a0 = (uint64_t)q.in & ~15ull;
+      const uint32_t nu = (uint32_t)((((uint64_t)q.in & 15) + q.fs + ex + 15) >> 4);
       if (w == 0) {
 #pragma unroll
-        for (uint32_t q = 0; q < PFX / 64; q++)
-          if (64 * q < nu && 64 * q + l < nu) dma16(a0 + 16ull * (64 * q + l), img + 1024 * q);
+        for (uint32_t u = 0; u < PFX / 64; u++)
+          if (64 * u < nu && 64 * u + l < nu) dma16(a0 + 16ull * (64 * u + l), img + 1024 * u);
       }
-      uint32_t after = 0;  // DMA instructions this wave issues after the prefix
+      uint32_t n = 0;
+      uint64_t src = a0 + 16ull * (PFX + 64 * w + l);  // (one address, stepped: registers)
 #pragma unroll
       for (uint32_t i = 0; i < (IMGU - PFX + NT - 1) / NT; i++) {
         const uint32_t u0 = PFX + 64 * (w + 16 * i);
         if (u0 < nu) {
-          after++;
-          if (u0 + l < nu) dma16(a0 + 16ull * (u0 + l), img + 16 * u0);
+          n++;
+          if (u0 + l < nu) dma16(src, img + 16 * u0);
         }
+        src += 16ull * NT;
       }
-      if (w == 0 && ABL != 1) {
-        // (vmcnt counts in issue order: the prefix has landed when at most
-        // `after` of this wave's DMA instructions are left)
-        switch (__builtin_amdgcn_readfirstlane(after)) {
-          case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-          case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-          case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-          case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-          default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        }
-        // (the parse is the one serial step of a tile: it issues first on its
-        // SIMD, ahead of the other workgroup's waves)
-        __builtin_amdgcn_s_setprio(3);
-        parse<SGN>(L, dk, l, chunked || mc);
-        __builtin_amdgcn_s_setprio(0);
+      return n;
+    };
+    // (multi-chunk) chunk k of the tile from the loop state; checked: a
+    // chunk this kernel decodes, inside the tile, and (the last one)
+    // completing the tile's unfiltered size (tile.cc:305-309)
+    auto chunk_desc = [&](uint32_t cur, uint32_t out_off, uint32_t ho, uint32_t hf, uint32_t hm, uint32_t kk,
+                          uint32_t nch, Desc& q, uint32_t& ex) -> bool {
+      const bool last = kk + 1 == nch;
+      const uint64_t cfs = 12ull + hm + hf;
+      ex = last ? 0u : 12u;
+      const uint64_t tin = ((uint64_t)__builtin_amdgcn_readfirstlane(L.mct[2]) << 32) |
+                           __builtin_amdgcn_readfirstlane(L.mct[1]);
+      const uint64_t tout = ((uint64_t)__builtin_amdgcn_readfirstlane(L.mct[4]) << 32) |
+                            __builtin_amdgcn_readfirstlane(L.mct[3]);
+      q.t = t;
+      q.fs = cfs;
+      q.os = ho;
+      q.in = (const uint8_t*)(tin + cur);
+      q.out = (uint8_t*)(tout + out_off);
+      return (uint64_t)cur + cfs + ex <= d.fs && ho >= 64 && ho <= OUTB && (ho & 3) == 0 && cfs + ex <= IMG_CAP &&
+             (uint64_t)out_off + ho <= d.os && (!last || (uint64_t)out_off + ho == d.os);
+    };
+    Desc dk = d;
+    uint32_t extra = 0;  // bytes DMA'd past the image: the next chunk's header
+    if (mc) {
+      auto S = [&](int i) -> uint32_t { return __builtin_amdgcn_readfirstlane(L.mcs[k & 1][i]); };
+      if (!chunk_desc(S(0), S(1), S(2), S(3), S(4), k, __builtin_amdgcn_readfirstlane(L.mct[0]), dk, extra)) {
+        declined = true;
+        break;
       }
     }
+    uint64_t* const pf = mc ? nullptr : prof;
+    if (!issued) {
+      after = __builtin_amdgcn_readfirstlane(issue_dma(dk, extra));
+      pend = 0;
+    }
+    if (w == 0 && ABL != 1) {
+      // (vmcnt counts in issue order: the prefix has landed when at most
+      // `after` DMA instructions and the `pend` stores behind them are left)
+      vm_wait(after + pend);
+      // (the parse is the one serial step of a tile: it issues first on its
+      // SIMD, ahead of the other workgroup's waves)
+      __builtin_amdgcn_s_setprio(3);
+      parse<SGN>(L, dk, l, chunked || mc);
+      __builtin_amdgcn_s_setprio(0);
+    }
     const uint64_t c1 = pf ? __builtin_amdgcn_s_memtime() : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait(pend);
     lds_barrier();
     const uint64_t c2 = pf ? __builtin_amdgcn_s_memtime() : 0;
     if (ABL != 1 && __builtin_amdgcn_readfirstlane(L.hd[0]) == 0) {
-      decline(kp, t);
-      return;
+      declined = true;
+      break;
     }
     const uint32_t wsh = __builtin_amdgcn_readfirstlane(L.hd[1]);
     const uint32_t b = (uint32_t)((uintptr_t)dk.in & 15);
     const uint32_t cb = __builtin_amdgcn_readfirstlane(L.hd[3]);
     const uint32_t wlast = __builtin_amdgcn_readfirstlane(L.hd[2]);
     const uint32_t nv = __builtin_amdgcn_readfirstlane(L.hd[7]);
-    if (mc && threadIdx.x == 0) {
-      // the loop state for the next chunk: its header (DMA'd behind this
-      // image; read before the end-of-chunk barrier lets the next DMA land)
+    // the next chunk (its header was DMA'd behind this image) and whether its
+    // DMA goes out before this chunk's stores
+    Desc dn = dk;
+    uint32_t extra_n = 0;
+    bool pipe = false;
+    if (mc && extra) {
       const uint32_t hb = b + (uint32_t)dk.fs;
-      if (extra) {
-        L.mcs[2] = rd32(L.IMG, hb);
-        L.mcs[3] = rd32(L.IMG, hb + 4);
-        L.mcs[4] = rd32(L.IMG, hb + 8);
+      const uint32_t nho = __builtin_amdgcn_readfirstlane(rd32(L.IMG, hb)),
+                     nhf = __builtin_amdgcn_readfirstlane(rd32(L.IMG, hb + 4)),
+                     nhm = __builtin_amdgcn_readfirstlane(rd32(L.IMG, hb + 8));
+      const uint32_t ncur = __builtin_amdgcn_readfirstlane(L.mcs[k & 1][0]) + (uint32_t)dk.fs,
+                     nout = __builtin_amdgcn_readfirstlane(L.mcs[k & 1][1]) + (uint32_t)dk.os;
+      pipe = chunk_desc(ncur, nout, nho, nhf, nhm, k + 1, __builtin_amdgcn_readfirstlane(L.mct[0]), dn, extra_n) &&
+             dk.os == OUTB;
+      // the next chunk's state, into the other buffer (read after the next
+      // barrier: the hook's, or the end of this chunk's)
+      if (threadIdx.x == 0) {
+        uint32_t* const m = L.mcs[(k + 1) & 1];
+        m[0] = ncur;
+        m[1] = nout;
+        m[2] = nho;
+        m[3] = nhf;
+        m[4] = nhm;
       }
-      L.mcs[0] += (uint32_t)dk.fs;
-      L.mcs[1] += (uint32_t)dk.os;
-      L.mcs[5] += 1;
     }
+    uint32_t after_n = 0;
+    // the next chunk's DMA, once every wave's reads of this chunk are issued
+    // and done (the barrier): before this chunk's stores
+    auto hook = [&]() {
+      if (!pipe) return;
+      lds_barrier();
+      after_n = __builtin_amdgcn_readfirstlane(issue_dma(dn, extra_n));
+    };
     if (cb != 0) {
       // coded DoubleDelta: one instantiation per code width
       switch (cb) {
 #define TDBG_CB(c) \
-  case c: coded_tile<c, SGN, ABL>(L, dk, b, wsh - 2, wlast, w, l, nv, pf); break;
+  case c: coded_tile<c, SGN, ABL, MC>(L, dk, b, wsh - 2, wlast, w, l, nv, pf, hook); break;
         TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
         TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
         TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
@@ -757,6 +830,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
 #undef TDBG_CB
         default: break;
       }
+      pend = 4;  // (pipelined: a full chunk's four unit rounds)
       if (pf && threadIdx.x == 0) {
         pf[0] = c1 - c0;
         pf[1] = c2 - c1;
@@ -774,14 +848,27 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       // such waves, for registers).  (Measured, not kept: the general rounds
       // first, one at a time, then all 16 one-read ranges together -- ramp
       // -0.9 %, rand -1.1 % on one box, profiles/r06/ab_general_first.txt.)
-      if (g.gen == 0 || ABL == 4) {
+      if (MC && pipe && g.gen == 0) {
+        // (pipelined: two halves of 8 ranges, the next chunk's DMA after the
+        // second half's reads -- 16 reads held through the DMA issue do not
+        // fit the registers)
+        decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
+        decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv, hook);
+        pend = 2;
+      } else if (g.gen == 0 || ABL == 4) {
         decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
+        hook();  // (a no-op unless pipelined)
+        pend = 0;
       } else if (ABL == 6) {
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv);
       } else {
         decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0, nv);
         decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2, nv);
+        // (such a wave -- a ramp tile's plane boundary -- takes part in the
+        // next chunk's DMA after its stores: registers)
+        hook();
+        pend = 0;
       }
       if (pf && l == 0) {
         const uint64_t c4 = __builtin_amdgcn_s_memtime();
@@ -797,7 +884,19 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       }
     }
     if (!mc || extra == 0) break;  // (the last chunk DMA'd no next header)
-    lds_barrier();  // every wave is done with this chunk's image, table and headers
+    if (!pipe) {
+      lds_barrier();  // every wave is done with this chunk's image, table and headers
+      pend = 0;
+    }
+    issued = pipe;
+    after = __builtin_amdgcn_readfirstlane(after_n);
+    pend = __builtin_amdgcn_readfirstlane(pend);
+  }
+  if (declined) {
+    // (a pipelined DMA may still be in flight into LDS: it drains before the
+    // workgroup ends; nothing reads it)
+    decline(kp, t);
+    return;
   }
   if (threadIdx.x == 0) {
     if (kp.status && !chunked) kp.status[t] = TDBG_OK;
@@ -813,7 +912,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         atomicAdd((unsigned long long*)&s[TDBG_STAT_FUSED_BYTES], (unsigned long long)d.os);
         atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_TILES], 1ull);
         if (any_raw && !mc) atomicAdd((unsigned long long*)&s[TDBG_STAT_STREAM_RAW_TILES], 1ull);
-        if (mc) atomicAdd((unsigned long long*)&s[TDBG_STAT_TILE_CHUNKS], (unsigned long long)L.mcs[6]);
+        if (mc) atomicAdd((unsigned long long*)&s[TDBG_STAT_TILE_CHUNKS], (unsigned long long)L.mct[0]);
       }
     }
   }
