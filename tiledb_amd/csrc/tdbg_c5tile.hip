@@ -735,10 +735,10 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       const bool last = kk + 1 == nch;
       const uint64_t cfs = 12ull + hm + hf;
       ex = last ? 0u : 12u;
-      const uint64_t tin = ((uint64_t)__builtin_amdgcn_readfirstlane(L.mct[2]) << 32) |
-                           __builtin_amdgcn_readfirstlane(L.mct[1]);
-      const uint64_t tout = ((uint64_t)__builtin_amdgcn_readfirstlane(L.mct[4]) << 32) |
-                            __builtin_amdgcn_readfirstlane(L.mct[3]);
+      // (the builtin returns int: each half goes through uint32_t, or a low
+      // half with its top bit set would be sign-extended over the high one)
+      auto u = [&](int i) -> uint64_t { return (uint32_t)__builtin_amdgcn_readfirstlane(L.mct[i]); };
+      const uint64_t tin = (u(2) << 32) | u(1), tout = (u(4) << 32) | u(3);
       q.t = t;
       q.fs = cfs;
       q.os = ho;
