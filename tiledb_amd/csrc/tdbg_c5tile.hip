@@ -604,7 +604,7 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
 // MC: the multi-chunk variant (launches flagged TDBG_MULTI_CHUNK): tiles of
 // several chunks are decoded chunk after chunk by their workgroup; without
 // it they are declined (the fused kernel takes them).
-template <bool SGN, int ABL, bool MC>
+template <bool SGN, int ABL, bool MC, bool PIPE = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
   __shared__ Lds L;
@@ -797,7 +797,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       const uint32_t ncur = __builtin_amdgcn_readfirstlane(L.mcs[k & 1][0]) + (uint32_t)dk.fs,
                      nout = __builtin_amdgcn_readfirstlane(L.mcs[k & 1][1]) + (uint32_t)dk.os;
       pipe = chunk_desc(ncur, nout, nho, nhf, nhm, k + 1, __builtin_amdgcn_readfirstlane(L.mct[0]), dn, extra_n) &&
-             dk.os == OUTB;
+             dk.os == OUTB && PIPE;
       // the next chunk's state, into the other buffer (read after the next
       // barrier: the hook's, or the end of this chunk's)
       if (threadIdx.x == 0) {
@@ -945,6 +945,14 @@ static hipError_t c5tile_grid(K k, const tdbg::KParams* kp, hipStream_t s) {
 // and spilled to scratch, which the counted vmcnt waits cannot allow.
 extern "C" hipError_t tdbg_launch_c5tile_mc(const tdbg::KParams* kp, int sgn, hipStream_t s) {
   using namespace tdbg::c5t;
+#ifdef TDBG_EXPERIMENTS
+  // A/B: the next chunk's DMA issued before this chunk's stores (measured
+  // slower: profiles/r06/c5big_pipe_ab.txt)
+  static const bool pipe = tdbg_hook("TDBG_C5T_PIPE") != nullptr;  // experiments
+  if (pipe)
+    return c5tile_grid(sgn ? unfilter_c5tile_kernel<true, 0, true, true> : unfilter_c5tile_kernel<false, 0, true, true>,
+                       kp, s);
+#endif
   return c5tile_grid(sgn ? unfilter_c5tile_kernel<true, 0, true> : unfilter_c5tile_kernel<false, 0, true>, kp, s);
 }
 #else

@@ -2,15 +2,16 @@
 # 4 MiB C5 tiles (64 chunks of 64 KiB), one box: tile mode with the tile
 # kernel's multi-chunk variant (chunk_parallel=None -> TDBG_MULTI_CHUNK) vs
 # the device chunk directory (True) vs the fused kernel (False).
-# usage: c5big_ab2.sh <tag>   (T=tiles, VARS=...)
+# usage: c5big_ab2.sh <tag>   (T=tiles, VARS=..., MODES="None True False",
+# ENVS="TDBG_LIB=... ..." for another library)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/c5big_${1:-x}
 mkdir -p $OUT
 cd $R
 for V in ${VARS:-active rand ramp}; do
-for CP in None True False; do
-  timeout -k 10 300 python -u - > $OUT/${V}_$CP.txt 2>&1 <<PY || { echo "failed $V $CP"; tail -20 $OUT/${V}_$CP.txt; exit 11; }
+for CP in ${MODES:-None True False}; do
+  env $ENVS timeout -k 10 300 python -u - > $OUT/${V}_$CP.txt 2>&1 <<PY || { echo "failed $V $CP"; tail -20 $OUT/${V}_$CP.txt; exit 11; }
 import sys, time, numpy as np, torch
 sys.path.insert(0, '.')
 import bench, workloads as W
