@@ -821,7 +821,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       // coded DoubleDelta: one instantiation per code width
       switch (cb) {
 #define TDBG_CB(c) \
-  case c: coded_tile<c, SGN, ABL, MC>(L, dk, b, wsh - 2, wlast, w, l, nv, pf, hook); break;
+  case c: coded_tile<c, SGN, ABL, MC && PIPE>(L, dk, b, wsh - 2, wlast, w, l, nv, pf, hook); break;
         TDBG_CB(2) TDBG_CB(3) TDBG_CB(4) TDBG_CB(5) TDBG_CB(6) TDBG_CB(7) TDBG_CB(8) TDBG_CB(9)
         TDBG_CB(10) TDBG_CB(11) TDBG_CB(12) TDBG_CB(13) TDBG_CB(14) TDBG_CB(15) TDBG_CB(16)
         TDBG_CB(17) TDBG_CB(18) TDBG_CB(19) TDBG_CB(20) TDBG_CB(21) TDBG_CB(22) TDBG_CB(23)
