@@ -144,6 +144,37 @@ def test_c5tile_coded_every_code_width(eng, ctx, oracle_mod):
     assert st == want, f"streaming kernel took {st}, expected {want}"
 
 
+def slope_values(rng, n: int = 16384) -> np.ndarray:
+    """Values whose byteshuffled stream is piecewise linear with nonzero
+    slopes: DD codes are zero along each segment (whole waves of them, which
+    the kernel's all-zero-codes path skips) while the running delta they
+    carry is not -- the skipped waves' values come from the fold alone."""
+    d = np.empty(n, dtype=np.int64)
+    i = 0
+    while i < n:
+        run = int(rng.integers(1500, 6000))
+        d[i:i + run] = int(rng.integers(-4000, 4000))
+        i += run
+    d[int(rng.integers(1, n))] = int(rng.integers(-50, 50))  # one isolated kink
+    s = np.cumsum(d) + int(rng.integers(-2**20, 2**20))
+    return unshuffle(s.astype(np.int32))
+
+
+def test_c5tile_coded_zero_code_waves(eng, ctx, oracle_mod):
+    """Whole waves of zero DD codes inside nonzero-slope segments, UINT32 and
+    INT32, next to step tiles: bit-exact, every tile taken by the kernel."""
+    rng = np.random.default_rng(27)
+    vals = [slope_values(rng) for _ in range(12)]
+    assert all(W.c5_dd_bitsize(v) < 31 for v in vals)
+    case = Case("c5_slopes", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
+    enc, fused, fb, st = _run(eng, ctx, oracle_mod, case)
+    assert fb == 0 and fused == len(enc)
+    assert st == len(enc), f"streaming kernel took {st} of {len(enc)} tiles"
+    case = Case("c5_slopes_u32", _pipe(), Datatype.UINT32, 4, [as_u8(v.view(np.uint32)) for v in vals[:4]])
+    enc, fused, fb, st = _run(eng, ctx, oracle_mod, case)
+    assert fb == 0 and st == len(enc)
+
+
 def test_c5tile_coded_uint32(eng, ctx, oracle_mod):
     """UINT32 (BWR zero-extends its 8/16-bit windows: spec 20)."""
     rng = np.random.default_rng(23)

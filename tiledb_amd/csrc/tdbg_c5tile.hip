@@ -461,6 +461,23 @@ __device__ __forceinline__ void coded_lane(Lds& L, uint32_t w, uint32_t l, uint3
     G[2 * x] = v.x;
     G[2 * x + 1] = v.y;
   }
+  // a wave whose codes are all zero (a constant-stride run: the common case
+  // in DD streams of run-heavy columns) skips the realignment, extraction
+  // and scan: every running sum and the wave's aggregate are 0 (wave 0 never
+  // does, its lane 0 injects the two header values)
+  uint32_t z = 0;
+#pragma unroll
+  for (int x = 0; x < 20; x++) z |= G[x];
+  if (__builtin_amdgcn_ballot_w64(z != 0 || w == 0) == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) xk[i] = 0;
+    ae = be = 0;
+    if (l == 63) {
+      L.red[w][0] = 0;
+      L.red[w][1] = 0;
+    }
+    return;
+  }
   uint32_t H[18];
 #pragma unroll
   for (int x = 0; x < 18; x++) H[x] = __builtin_amdgcn_alignbyte(G[x + 1], G[x], 2);
