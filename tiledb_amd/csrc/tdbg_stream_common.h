@@ -217,22 +217,25 @@ __device__ __forceinline__ WinTab bwr_window_table(const uint32_t* P, uint2* TAB
 // BWR^-1 of a whole chunk's stream (bit_width_reduction_filter.cc:353-404)
 // into LDS, in place over the image, in 16-B units of 4 elements: thread T of
 // a 1,024-thread workgroup decodes units T + 1024 j (j < 4: at most 64 KiB of
-// output; rounds whose units all lie past nun units are skipped, a
-// wave-uniform test).  A unit's 4 elements lie in one window (windows are >=
-// 64 elements), looked up per lane (esh = log2(elements per window), wlast =
+// output).  A unit's 4 elements lie in one window (windows are >= 64
+// elements), looked up per lane (esh = log2(elements per window), wlast =
 // the last window).  Per round one wave-uniform decoder: every lane's window
 // 8-bit (one dword read gives the unit), or the general form (five dwords
 // realigned, then per element the window's kind: raw dword, 8-bit byte or
 // 16-bit half, plus the minimum).  Every compressed read lands in registers
 // before the one barrier after which the decoded units overwrite the image.
-template <bool SGN>
-__device__ __forceinline__ void bwr_materialize(uint32_t* IMG, const uint2* TAB, uint32_t b, uint32_t esh,
-                                                uint32_t wlast, uint32_t w, uint32_t l, uint32_t nun) {
-  v4u dv[4];
-  uint2 te[4];
-  uint32_t ea[4];
+// NR: the wave's rounds with a unit below nun (all of them lie in the chunk),
+// one instantiation each -- a round skipped behind a branch left its
+// registers to be zeroed at every exit (40 VALU per wave, measured in the
+// ISA); every path holds exactly one barrier.
+template <bool SGN, int NR>
+__device__ __forceinline__ void bwr_materialize_n(uint32_t* IMG, const uint2* TAB, uint32_t b, uint32_t esh,
+                                                  uint32_t wlast, uint32_t w, uint32_t l) {
+  v4u dv[NR];
+  uint2 te[NR];
+  uint32_t ea[NR];
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
+  for (uint32_t j = 0; j < NR; j++) {
     const uint32_t e = 4 * (1024 * j + 64 * w + l);
     uint32_t W = e >> esh;
     W = W < wlast ? W : wlast;
@@ -240,19 +243,17 @@ __device__ __forceinline__ void bwr_materialize(uint32_t* IMG, const uint2* TAB,
     const uint32_t kind = te[j].x >> 20;
     ea[j] = (te[j].x & OFFM) + b + ((e - (W << esh)) << kind);  // LDS byte of element e's compressed value
   }
-  // (every round's five dwords first, so that all 20 reads are in flight
+  // (every round's five dwords first, so that all the reads are in flight
   // together; the decoders below pick from them)
-  uint32_t D[4][5];
+  uint32_t D[NR][5];
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
+  for (uint32_t j = 0; j < NR; j++) {
     const uint32_t* p = IMG + (ea[j] >> 2);
 #pragma unroll
     for (int k = 0; k < 5; k++) D[j][k] = p[k];
   }
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
+  for (uint32_t j = 0; j < NR; j++) {
     const uint32_t kind = te[j].x >> 20, mn = te[j].y, sh = ea[j] & 3;
     if (__builtin_amdgcn_ballot_w64(kind != 0) == 0) {
       const uint32_t y = __builtin_amdgcn_alignbyte(D[j][1], D[j][0], sh);
@@ -271,9 +272,20 @@ __device__ __forceinline__ void bwr_materialize(uint32_t* IMG, const uint2* TAB,
   }
   lds_barrier();  // every compressed byte is in registers: the stream may overwrite the image
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (1024 * j + 64 * w >= nun) break;
-    *(v4u*)(IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+  for (uint32_t j = 0; j < NR; j++) *(v4u*)(IMG + 4 * (1024 * j + 64 * w + l)) = dv[j];
+}
+
+template <bool SGN>
+__device__ __forceinline__ void bwr_materialize(uint32_t* IMG, const uint2* TAB, uint32_t b, uint32_t esh,
+                                                uint32_t wlast, uint32_t w, uint32_t l, uint32_t nun) {
+  // (wave-uniform: round j has a unit below nun iff 1024 j + 64 w < nun)
+  const uint32_t nr = nun <= 64 * w ? 0u : min(4u, (nun - 64 * w + 1023) >> 10);
+  switch (__builtin_amdgcn_readfirstlane(nr)) {
+    case 4: bwr_materialize_n<SGN, 4>(IMG, TAB, b, esh, wlast, w, l); break;
+    case 3: bwr_materialize_n<SGN, 3>(IMG, TAB, b, esh, wlast, w, l); break;
+    case 2: bwr_materialize_n<SGN, 2>(IMG, TAB, b, esh, wlast, w, l); break;
+    case 1: bwr_materialize_n<SGN, 1>(IMG, TAB, b, esh, wlast, w, l); break;
+    default: lds_barrier(); break;
   }
 }
 
