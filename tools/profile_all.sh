@@ -13,7 +13,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin" [c5big]="active" [c5s]="active rand ramp" [c5shard]="active rand ramp")
+declare -A VARS=([c1]="ramp rand" [c2]="sin" [c2i]="sin" [c3a]="coords" [c3b]="coords" [c4]="offsets" [c5]="active rand ramp" [xor]="sin" [delta]="active" [fscale]="sin" [c5big]="active rand ramp" [c5s]="active rand ramp" [c5shard]="active rand ramp")
 for CFG in $CFGS; do
   # c5shard: C5 on one GPU's shard of the 8-GPU config (12,500 tiles)
   if [ $CFG = c5shard ]; then CA="--config c5 --tiles-per-gpu 12500"; else CA="--config $CFG"; fi

@@ -69,7 +69,9 @@ def main(out):
         lines = [l for l in open(log) if l.startswith("{")]
         if not lines:
             continue
-        line = json.loads(lines[-1])
+        # (the full line, not the compact one printed after it: its variants
+        # carry their own algorithmic bytes)
+        line = json.loads(max(lines, key=len))
         variants = line["config"].get("variants") or {line["config"]["variant"]: {}}
         for v in variants:
             key = f"{cfg}_{v}"
