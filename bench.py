@@ -824,7 +824,7 @@ def compact_line(line: dict, legs_file) -> dict:
         cc["other_configs"] = oc
     if "c3_combined" in c:
         cc["c3_combined"] = {k: c["c3_combined"][k] for k in ("GiBps", "roofline_frac")}
-    for leg in ("c5_shard_12500", "c5_40000B_tiles", "c5_4MiB_tiles"):
+    for leg in ("c5_shard_12500", "c5_40000B_tiles", "c5_4MiB_tiles", "c5_dense_codes"):
         if leg in c:
             cc[leg] = {v: {"GiBps": x["GiBps"], "roofline_frac": x["roofline_frac"],
                            "ms_per_step": x["ms_per_step"], "kernel_ms": x["kernel_ms"]}
@@ -895,6 +895,8 @@ def main():
                     help="N = 1 run: also time the C5 pipeline on 40,000-B tiles (0 = skip)")
     ap.add_argument("--c5big-tiles", type=int, default=CONFIGS["c5big"]["tiles_per_gpu"],
                     help="N = 1 run: also time the C5 pipeline on 4 MiB tiles, tile mode (0 = skip)")
+    ap.add_argument("--dense-tiles", type=int, default=100000,
+                    help="C5 tiles of dense DoubleDelta codes (variant 'walk') for the c5_dense_codes leg (0: off)")
     ap.add_argument("--legs-file", default="gpurun_out/bench_legs.json",
                     help="every leg's full JSON (also printed on the line before the headline); '' = none")
     args = ap.parse_args()
@@ -1009,6 +1011,19 @@ def main():
                 "workload": CONFIGS["c5big"]["workload"], "tiles": args.c5big_tiles, "steps": args.steps,
                 "kernel": kernel_name("c5big", cres[variants[0]]), "variants": sb,
                 "min_over_variants_roofline_frac": round(min(x["roofline_frac"] for x in sb.values()), 4)}
+        # the C5 pipeline with dense DoubleDelta codes (variant 'walk', not a
+        # BASELINE variant): the coded path when no wave's codes are all zero
+        # (the active tiles skip 11 of 16 waves' code extraction)
+        if args.dense_tiles:
+            _, dres = run_config(engine, ctx, W, args, "c5", ["walk"], args.dense_tiles, args.steps,
+                                 args.warmup, dist, world, rank)
+            dv = variant_line("c5", "walk", dres["walk"], world)
+            dres["walk"].pop("packed", None)
+            line["config"]["c5_dense_codes"] = {
+                "workload": "C5 pipeline, 64 KiB tiles whose byteshuffled stream is a random walk (steps "
+                            "U{-500..500}): DoubleDelta bit-packed at bitsize 10 with nonzero codes throughout, "
+                            "BWR windows over DD's output raw (23,415 B filtered)",
+                "tiles": args.dense_tiles, "steps": args.steps, "variants": {"walk": dv}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # after every timed region, at N = 1 only (the N > 1 lines divide the
         # same job over more GPUs; the CPU figure does not change with N)

@@ -175,6 +175,17 @@ def test_c5tile_coded_zero_code_waves(eng, ctx, oracle_mod):
     assert fb == 0 and st == len(enc)
 
 
+def test_c5tile_coded_dense_codes(eng, ctx, oracle_mod):
+    """The bench's 'walk' tiles (c5_dense_codes leg): nonzero DD codes in
+    every wave, BWR windows raw; every tile taken, bit-exact."""
+    pool, vals = W.c5_pool("walk", 16, seed=28)
+    assert all(W.c5_dd_bitsize(v) < 31 for v in vals)
+    case = Case("c5_walk", _pipe(), Datatype.INT32, 4, [as_u8(v) for v in vals])
+    enc, fused, fb, st = _run(eng, ctx, oracle_mod, case)
+    assert fb == 0 and fused == len(enc)
+    assert st == len(enc), f"streaming kernel took {st} of {len(enc)} tiles"
+
+
 def test_c5tile_coded_uint32(eng, ctx, oracle_mod):
     """UINT32 (BWR zero-extends its 8/16-bit windows: spec 20)."""
     rng = np.random.default_rng(23)

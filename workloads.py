@@ -396,7 +396,18 @@ def c5_values(variant: str, tile_index: int, rng: np.random.Generator, n: int = 
     active: a low-cardinality step column (runs of U{256..2047} equal values,
             values U{0..15}): all three stages do work -- DoubleDelta bitsize 28
             (< 31: the bit-packed path), ~92 % of the BWR windows over DD's
-            output 8-bit, byteshuffle over the whole tile (~20 KB filtered)."""
+            output 8-bit, byteshuffle over the whole tile (~20 KB filtered).
+    walk:   dense codes -- the byteshuffled stream is a random walk (steps
+            U{-500..500}), so DoubleDelta codes are nonzero almost everywhere
+            (the bit-packed path with no all-zero wave) and the BWR windows over
+            DD's output are mostly raw.  Not a BASELINE variant: the bench's
+            c5_dense_codes leg, the coded path's rate when no wave can skip its
+            codes."""
+    if variant == "walk":
+        steps = rng.integers(-500, 501, n).astype(np.int64)
+        s = (np.cumsum(steps) + int(rng.integers(-2**20, 2**20))).astype(np.int32)
+        # the values whose 4-byte byteshuffle is s
+        return s.astype("<i4").view(np.uint8).reshape(4, n).T.reshape(-1).view("<i4").copy()
     if variant == "ramp":
         return (np.arange(n, dtype=np.int64) + tile_index * n).astype(np.int32)
     if variant == "rand":
