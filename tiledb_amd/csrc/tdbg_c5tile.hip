@@ -321,7 +321,11 @@ __device__ __forceinline__ void store_unit(uint8_t* p, const v4u& v, uint32_t u,
 struct NoHook {
   __device__ __forceinline__ void operator()() const {}
 };
-template <bool SGN, int ABL, bool GEN, int NR, typename Hook = NoHook>
+// FULL: a full 64 KiB chunk (no per-round test, whole-unit stores without a
+// lane test); RAW: every range of the wave raw (every rand wave): no
+// per-range decoder branch.  (Both measured: the branch-free all-raw full
+// path rand 0.739 -> 0.757, same box, profiles/r06/ab_rawf.txt.)
+template <bool SGN, int ABL, bool GEN, int NR, typename Hook = NoHook, bool FULL = false, bool RAW = false>
 __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint32_t b, uint32_t w, uint32_t l,
                                              uint8_t* o, uint32_t r0, uint32_t nv, const Hook& hook = Hook()) {
   uint32_t y[NR];
@@ -330,7 +334,7 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
     const uint32_t i = 4 * r0 + j;
     const uint32_t Q0 = 26 + nv * (i & 3) + 4 * (1024 * (i >> 2) + 64 * w);
     const uint32_t e = (Q0 >> 2) + l;
-    uint32_t a = __builtin_amdgcn_readlane(g.base, i) + (((g.is8 >> i) & 1) ? l : 4 * l);
+    uint32_t a = __builtin_amdgcn_readlane(g.base, i) + ((!RAW && ((g.is8 >> i) & 1)) ? l : 4 * l);
     if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b, Q0 & 3);
     y[j] = (ABL == 1 || ABL == 2) ? l + i : rd32(L.IMG, a);
   }
@@ -338,13 +342,13 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
 #pragma unroll
   for (uint32_t rr = 0; rr < NR / 4; rr++) {
     const uint32_t r = r0 + rr;
-    if (1024 * r + 64 * w >= ((nv + 3) >> 2)) break;  // (wave-uniform: no unit of this round is in the chunk)
+    if (!FULL && 1024 * r + 64 * w >= ((nv + 3) >> 2)) break;  // (wave-uniform: no unit of this round is in the chunk)
     uint32_t x[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
       const uint32_t i = 4 * r + k;
       x[k] = y[4 * rr + k];
-      if (ABL == 1 || ABL == 2 || ABL == 5) continue;
+      if (RAW || ABL == 1 || ABL == 2 || ABL == 5) continue;
       const uint32_t Q0 = 26 + nv * k + 4 * (1024 * r + 64 * w);
       const uint32_t e = (Q0 >> 2) + l, sk = Q0 & 3;
       // (wave-uniform branches: all 16 reads are already in flight)
@@ -358,7 +362,9 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
       }
     }
     const v4u v = unshuffle4(x);
-    if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
+    if (FULL && ABL == 0)
+      __builtin_nontemporal_store((v4a)v, (g_a4*)(o + 16384u * r));
+    else if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
       store_unit(o + 16384u * r, v, 1024 * r + 64 * w + l, nv);
   }
 }
@@ -872,6 +878,14 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv, hook);
         pend = 2;
+      } else if (ABL == 0 && g.gen == 0 && g.is8 == 0 && nv == OUTB / 4) {
+        decode_store<SGN, ABL, false, 16, NoHook, true, true>(L, g, b, w, l, o, 0, nv);
+        hook();  // (a no-op unless pipelined)
+        pend = 0;
+      } else if (ABL == 0 && g.gen == 0 && nv == OUTB / 4) {
+        decode_store<SGN, ABL, false, 16, NoHook, true>(L, g, b, w, l, o, 0, nv);
+        hook();
+        pend = 0;
       } else if (g.gen == 0 || ABL == 4) {
         decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
         hook();  // (a no-op unless pipelined)
@@ -879,6 +893,11 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       } else if (ABL == 6) {
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 0, nv);
         decode_store<SGN, ABL, false, 8>(L, g, b, w, l, o, 2, nv);
+      } else if (ABL == 0 && nv == OUTB / 4) {
+        decode_store<SGN, ABL, true, 8, NoHook, true>(L, g, b, w, l, o, 0, nv);
+        decode_store<SGN, ABL, true, 8, NoHook, true>(L, g, b, w, l, o, 2, nv);
+        hook();
+        pend = 0;
       } else {
         decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 0, nv);
         decode_store<SGN, ABL, true, 8>(L, g, b, w, l, o, 2, nv);
