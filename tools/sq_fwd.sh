@@ -15,5 +15,5 @@ for SET in "$A" "$C"; do
   P=$((P+1))
   timeout -s KILL 120 rocprofv3 --pmc $SET --output-format csv -d $OUT/sq_fwd/pass$P -o run -- python3 $R/bench.py $B > $OUT/sq_fwd_$P.log 2>&1 || { echo "sq pass $P failed"; tail -20 $OUT/sq_fwd_$P.log; exit 12; }
 done
-TDBG_KNAME="filter_stream_c5_kernel" python3 $R/tools/sq_summary.py $OUT/sq_fwd c5 active > $OUT/sq_fwd.json || exit 13
+TDBG_KNAME="${KN:-fws::filter_c5tile_kernel}" python3 $R/tools/sq_summary.py $OUT/sq_fwd c5 active > $OUT/sq_fwd.json || exit 13
 python3 -c "import json; d=json.load(open('$OUT/sq_fwd.json')); print(json.dumps(d['derived']))"
