@@ -1,0 +1,7 @@
+#!/bin/bash
+# BWR materialization: an all-raw-windows round path (dense-code tiles) A/B
+set -o pipefail
+mkdir -p gpurun_out/matraw
+timeout -k 10 300 python -u -m pytest tests/test_gpu_c5tile.py tests/test_gpu_c5_shapes.py tests/test_gpu_c2tile.py -x -q --timeout 120 --timeout-method thread > gpurun_out/matraw/t.log 2>&1 || { tail -30 gpurun_out/matraw/t.log; exit 11; }
+tail -1 gpurun_out/matraw/t.log
+VARS="walk active" bash tools/ab_lib.sh matraw_c5
