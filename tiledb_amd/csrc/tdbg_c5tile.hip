@@ -303,8 +303,12 @@ __device__ __forceinline__ uint32_t gen_dword(const GenRange& q, uint32_t e, uin
 // (a chunk of a multi-chunk tile starts at a multiple of its size).
 typedef uint32_t v4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
 typedef __attribute__((address_space(1))) v4a g_a4;
-__device__ __forceinline__ void store_unit(uint8_t* p, const v4u& v, uint32_t u, uint32_t nv) {
-  if (u < (nv >> 2)) {
+__device__ __forceinline__ void store_unit(uint8_t* p, const v4u& v, uint32_t u, uint32_t nv, bool whole) {
+  // (whole: the wave's 64 units all lie below nv / 4 -- a wave-uniform test
+  // that keeps the lane test to the one wave-round holding the chunk's end)
+  if (whole) {
+    __builtin_nontemporal_store((v4a)v, (g_a4*)p);
+  } else if (u < (nv >> 2)) {
     __builtin_nontemporal_store((v4a)v, (g_a4*)p);
   } else if (u < ((nv + 3) >> 2)) {
     uint32_t* q = (uint32_t*)p;
@@ -365,7 +369,7 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
     if (FULL && ABL == 0)
       __builtin_nontemporal_store((v4a)v, (g_a4*)(o + 16384u * r));
     else if (ABL != 3 || (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u))
-      store_unit(o + 16384u * r, v, 1024 * r + 64 * w + l, nv);
+      store_unit(o + 16384u * r, v, 1024 * r + 64 * w + l, nv, 1024 * r + 64 * w + 64 <= (nv >> 2));
   }
 }
 
@@ -602,7 +606,7 @@ __device__ __forceinline__ void coded_tile(Lds& L, const Desc& d, uint32_t b, ui
           x[k] = __builtin_amdgcn_alignbyte(L.IMG[vslot(v0 + 1)], L.IMG[vslot(v0)], (nv * k) & 3);
       }
       const v4u v = unshuffle4(x);
-      store_unit(o + 16384u * r, v, 1024 * r + T, nv);
+      store_unit(o + 16384u * r, v, 1024 * r + T, nv, 1024 * r + 64 * w + 64 <= (nv >> 2));
     }
   }
   if (prof && l == 0 && (w == 0 || w == 15)) {
