@@ -625,7 +625,7 @@ OTHER_CONFIGS = ("c1", "c2", "c2i", "c3a", "c3b", "c4")
 
 
 FORWARD_KERNEL = {
-    "c5": "filter_stream_c5_kernel (tdbg_forward_stream.hip) + filter_tiles_kernel on its queue",
+    "c5": "filter_c5tile_kernel (tdbg_forward_stream.hip, one 1,024-thread workgroup per tile) + filter_tiles_kernel on its queue",
     "c3a": "filter_small_kernel<0> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
     "c3b": "filter_small_kernel<1> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
     "c4": "filter_small_kernel<2> (tdbg_forward_small.hip) + filter_tiles_kernel on its queue",
