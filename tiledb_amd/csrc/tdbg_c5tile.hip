@@ -890,6 +890,11 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         decode_store<SGN, ABL, false, 16, NoHook, true>(L, g, b, w, l, o, 0, nv);
         hook();
         pend = 0;
+      } else if (ABL == 0 && g.gen == 0 && g.is8 == 0) {
+        // (all raw in a shorter chunk: no per-range decoder branch)
+        decode_store<SGN, ABL, false, 16, NoHook, false, true>(L, g, b, w, l, o, 0, nv);
+        hook();
+        pend = 0;
       } else if (g.gen == 0 || ABL == 4) {
         decode_store<SGN, ABL, false, 16>(L, g, b, w, l, o, 0, nv);
         hook();  // (a no-op unless pipelined)

@@ -1,0 +1,8 @@
+#!/bin/bash
+# wave-uniform rawp-unit stores in partial chunks (40,000-B tiles) A/B
+set -o pipefail
+mkdir -p gpurun_out/rawp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_c5tile.py tests/test_gpu_c5_shapes.py -x -q --timeout 120 --timeout-method thread > gpurun_out/rawp/t.log 2>&1 || { tail -30 gpurun_out/rawp/t.log; exit 11; }
+tail -1 gpurun_out/rawp/t.log
+VARS="rand" CFG=c5s bash tools/ab_lib.sh rawp_c5s &&
+VARS="rand" bash tools/ab_lib.sh rawp_c5
