@@ -329,7 +329,10 @@ struct NoHook {
 // lane test); RAW: every range of the wave raw (every rand wave): no
 // per-range decoder branch.  (Both measured: the branch-free all-raw full
 // path rand 0.739 -> 0.757, same box, profiles/r06/ab_rawf.txt.)
-template <bool SGN, int ABL, bool GEN, int NR, typename Hook = NoHook, bool FULL = false, bool RAW = false>
+// PAT >= 0: the wave's 8-bit ranges are planes k with bit k of PAT set, in every round (a constant
+// high byte plane's windows: ramp-like columns) -- the decoder per range is fixed at compile time.
+template <bool SGN, int ABL, bool GEN, int NR, typename Hook = NoHook, bool FULL = false, bool RAW = false,
+          int PAT = -1>
 __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint32_t b, uint32_t w, uint32_t l,
                                              uint8_t* o, uint32_t r0, uint32_t nv, const Hook& hook = Hook()) {
   uint32_t y[NR];
@@ -338,7 +341,8 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
     const uint32_t i = 4 * r0 + j;
     const uint32_t Q0 = 26 + nv * (i & 3) + 4 * (1024 * (i >> 2) + 64 * w);
     const uint32_t e = (Q0 >> 2) + l;
-    uint32_t a = __builtin_amdgcn_readlane(g.base, i) + ((!RAW && ((g.is8 >> i) & 1)) ? l : 4 * l);
+    const bool r8 = PAT >= 0 ? ((PAT >> (i & 3)) & 1) != 0 : (!RAW && ((g.is8 >> i) & 1));
+    uint32_t a = __builtin_amdgcn_readlane(g.base, i) + (r8 ? l : 4 * l);
     if (GEN && ((g.gen >> i) & 1)) a = gen_addr(gen_range(g, i), e, b, Q0 & 3);
     y[j] = (ABL == 1 || ABL == 2) ? l + i : rd32(L.IMG, a);
   }
@@ -356,7 +360,14 @@ __device__ __forceinline__ void decode_store(const Lds& L, const Ranges& g, uint
       const uint32_t Q0 = 26 + nv * k + 4 * (1024 * r + 64 * w);
       const uint32_t e = (Q0 >> 2) + l, sk = Q0 & 3;
       // (wave-uniform branches: all 16 reads are already in flight)
-      if ((g.is8 >> i) & 1) {
+      if (PAT >= 0) {
+        if ((PAT >> k) & 1) {
+          const uint32_t m0 = __builtin_amdgcn_readlane(g.m0, i), m1 = __builtin_amdgcn_readlane(g.m1, i),
+                         e1 = __builtin_amdgcn_readlane(g.e1, i);
+          const uint32_t v0 = ext<SGN>(x[k], 0, 8) + (e < e1 ? m0 : m1), v1 = ext<SGN>(x[k], 8, 8) + (e + 1 < e1 ? m0 : m1);
+          x[k] = __builtin_amdgcn_alignbyte(v1, v0, sk);
+        }
+      } else if ((g.is8 >> i) & 1) {
         const uint32_t m0 = __builtin_amdgcn_readlane(g.m0, i), m1 = __builtin_amdgcn_readlane(g.m1, i),
                        e1 = __builtin_amdgcn_readlane(g.e1, i);
         const uint32_t v0 = ext<SGN>(x[k], 0, 8) + (e < e1 ? m0 : m1), v1 = ext<SGN>(x[k], 8, 8) + (e + 1 < e1 ? m0 : m1);
@@ -887,7 +898,14 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         hook();  // (a no-op unless pipelined)
         pend = 0;
       } else if (ABL == 0 && g.gen == 0 && nv == OUTB / 4) {
-        decode_store<SGN, ABL, false, 16, NoHook, true>(L, g, b, w, l, o, 0, nv);
+        // (the common plane patterns of 8-bit ranges: decoders fixed at compile time)
+        switch (g.is8) {
+          case 0xCCCCu: decode_store<SGN, ABL, false, 16, NoHook, true, false, 0xC>(L, g, b, w, l, o, 0, nv); break;
+          case 0x8888u: decode_store<SGN, ABL, false, 16, NoHook, true, false, 0x8>(L, g, b, w, l, o, 0, nv); break;
+          case 0xEEEEu: decode_store<SGN, ABL, false, 16, NoHook, true, false, 0xE>(L, g, b, w, l, o, 0, nv); break;
+          case 0xFFFFu: decode_store<SGN, ABL, false, 16, NoHook, true, false, 0xF>(L, g, b, w, l, o, 0, nv); break;
+          default: decode_store<SGN, ABL, false, 16, NoHook, true>(L, g, b, w, l, o, 0, nv); break;
+        }
         hook();
         pend = 0;
       } else if (ABL == 0 && g.gen == 0 && g.is8 == 0) {
