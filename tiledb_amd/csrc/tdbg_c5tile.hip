@@ -250,15 +250,18 @@ __device__ __forceinline__ Ranges setup_ranges(const Lds& L, uint32_t b, uint32_
   g.m1 = t1.y;
   g.e0 = W0 << esh;
   g.e1 = W1 > W0 ? W1 << esh : 0xffffffffu;
-  {
-    const uint32_t y = rd32(L.IMG, (t1.x & OFFM) + b);
-    g.s1 = k1 == 2 ? y : (k1 == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + t1.y;
-  }
   g.base = !valid ? 0u
            : raw  ? (t0.x & OFFM) + (Q0 - (W0 << wsh)) + b
                   : (t0.x & OFFM) + ((Q0 >> 2) - (W0 << esh)) + b;
   g.is8 = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && valid && b8);
   g.gen = (uint32_t)__builtin_amdgcn_ballot_w64(l < 16 && valid && !raw && !b8);
+  // W1's first element decoded: only the general decoder uses it (a second
+  // dependent LDS round trip the other waves skip)
+  g.s1 = 0;
+  if (g.gen != 0) {
+    const uint32_t y = rd32(L.IMG, (t1.x & OFFM) + b);
+    g.s1 = k1 == 2 ? y : (k1 == 0 ? ext<SGN>(y, 0, 8) : ext<SGN>(y, 0, 16)) + t1.y;
+  }
   return g;
 }
 
