@@ -881,9 +881,12 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
       const Ranges g = setup_ranges<SGN>(L, b, w, l, wsh, wlast, nv);
       uint8_t* const o = dk.out + 16u * (64 * w + l);
       // (the wave's ranges inside the chunk: rounds r with 1024 r + 64 w < nv / 4)
-      const uint32_t nu4 = (nv + 3) >> 2;
-      const uint32_t vr = nu4 <= 64 * w ? 0u : min(4u, (nu4 - 64 * w + 1023) >> 10);
-      const uint32_t vmask = vr >= 4 ? 0xFFFFu : (1u << (4 * vr)) - 1u;
+      uint32_t vmask = 0;
+      if constexpr (!PIPE) {
+        const uint32_t nu4 = (nv + 3) >> 2;
+        const uint32_t vr = nu4 <= 64 * w ? 0u : min(4u, (nu4 - 64 * w + 1023) >> 10);
+        vmask = vr >= 4 ? 0xFFFFu : (1u << (4 * vr)) - 1u;
+      }
       const uint64_t c3 = pf ? __builtin_amdgcn_s_memtime() + (uint64_t)(g.x0 & 0) : 0;
       // All 16 ranges' reads first, then the decode and one store per round.
       // Raw and 8-bit ranges read one dword (the decoder picked by a select).
@@ -920,7 +923,7 @@ unfilter_c5tile_kernel(const KParams kp, uint32_t base, uint32_t cnt) {
         decode_store<SGN, ABL, false, 16, NoHook, false, true>(L, g, b, w, l, o, 0, nv);
         hook();
         pend = 0;
-      } else if (ABL == 0 && g.gen == 0 && g.is8 != 0 &&
+      } else if (ABL == 0 && !PIPE && g.gen == 0 && g.is8 != 0 &&
                  (g.is8 == (0xCCCCu & vmask) || g.is8 == (0x8888u & vmask))) {
         // (shorter chunks: the plane patterns over the wave's rounds inside the chunk)
         if (g.is8 == (0xCCCCu & vmask)) decode_store<SGN, ABL, false, 16, NoHook, false, false, 0xC>(L, g, b, w, l, o, 0, nv);
